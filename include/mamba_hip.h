@@ -1,0 +1,164 @@
+/*
+ * mamba_hip.h — C ABI of the MI355X many-chain MCMC engine (libmambahip.so).
+ *
+ * Drop-in boundary: this library replaces, for the supported
+ * lowered models, everything Mamba.jl runs under `pmap2(mcmc_worker!, lsts)`
+ * in `mcmc_master!`:
+ *   /root/reference/src/model/mcmc.jl:36-59   mcmc_master!  (chain fan-out)
+ *   /root/reference/src/model/mcmc.jl:62-83   mcmc_worker!  (per-chain loop, keep rule)
+ *   /root/reference/src/model/simulation.jl:93-107  sample!(m)  (block sweep)
+ *   /root/reference/src/samplers/{amwg,amm,nuts,slice}.jl  (block updates)
+ *   /root/reference/src/model/simulation.jl:47-90   logpdf! / gradlogpdf!
+ * A Julia `ccall` shim binds these symbols from a specialised
+ * mcmc_master!; unsupported models/schemes return MMB_E_UNSUPPORTED so the
+ * shim can fall back to the Julia path.
+ *
+ * Conventions: every function returns 0 on success or a negative MMB_E* code
+ * (message via mmb_last_error); nothing throws across the ABI.  All real
+ * arrays are FP64 (Mamba is Float64-only, src/Mamba.jl:57-58).  Host buffers
+ * are caller-owned; device memory is owned by the engine.  An engine is used by
+ * one host thread at a time (one engine per GPU; multi-GPU = one process per
+ * GPU, each with its own shard of global chain ids).
+ */
+#ifndef MAMBA_HIP_H
+#define MAMBA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMB_ABI_VERSION 1
+#define MMB_MAX_BLOCKS 8
+#define MMB_MAX_NODES_PER_BLOCK 4
+
+/* ---- error codes ---- */
+#define MMB_OK 0
+#define MMB_E_ARG (-1)         /* invalid argument (ArgumentError in mcmc.jl:22-25, amwg.jl:37-42) */
+#define MMB_E_UNSUPPORTED (-2) /* model/scheme not lowered to a kernel: fall back to Julia */
+#define MMB_E_HIP (-3)         /* HIP runtime error */
+#define MMB_E_STATE (-4)       /* call out of order (e.g. run before init) */
+#define MMB_E_NOMEM (-5)
+
+/* ---- lowered model kinds ---- */
+typedef enum {
+  MMB_MODEL_LINE = 1,    /* doc/tutorial/line.jl:5-25   y ~ IsoNormal(xmat*beta, sqrt(s2)) */
+  MMB_MODEL_RATS = 2,    /* doc/examples/rats.jl:48-97  hierarchical growth model */
+  MMB_MODEL_LOGISTIC = 3 /* build-defined:  y ~ Bernoulli(invlogit(X*beta)) */
+} mmb_model_kind;
+
+/* node ids (Stochastic nodes that can appear in a sampling block) */
+enum { MMB_LINE_BETA = 0, MMB_LINE_S2 = 1 };
+enum {
+  MMB_RATS_S2_C = 0, MMB_RATS_ALPHA = 1, MMB_RATS_MU_ALPHA = 2, MMB_RATS_S2_ALPHA = 3,
+  MMB_RATS_BETA = 4, MMB_RATS_MU_BETA = 5, MMB_RATS_S2_BETA = 6
+};
+enum { MMB_LOGISTIC_BETA = 0 };
+
+/* ---- sampler kinds (src/samplers/{amwg,amm,nuts,slice}.jl) ---- */
+typedef enum {
+  MMB_SAMPLER_AMWG = 1,  /* src/samplers/amwg.jl:47-61 */
+  MMB_SAMPLER_AMM = 2,   /* src/samplers/amm.jl:160-174 */
+  MMB_SAMPLER_NUTS = 3,  /* src/samplers/nuts.jl:47-56 */
+  MMB_SAMPLER_SLICE = 4, /* src/samplers/slice.jl:252-263 */
+  MMB_SAMPLER_GIBBS = 5  /* user Sampler(params, f): conjugate full conditional of the block's node,
+                            e.g. doc/tutorial/line.jl:168-186 */
+} mmb_sampler_kind;
+
+typedef enum { MMB_ADAPT_ALL = 0, MMB_ADAPT_BURNIN = 1, MMB_ADAPT_NONE = 2 } mmb_adapt;
+typedef enum { MMB_SLICE_MULTIVARIATE = 0, MMB_SLICE_UNIVARIATE = 1 } mmb_slice_form;
+
+/* One sampling block = one Sampler in Model.samplers (src/Mamba.jl:119-124). */
+typedef struct {
+  int32_t sampler;                         /* mmb_sampler_kind */
+  int32_t nnodes;                          /* number of nodes in `params` */
+  int32_t nodes[MMB_MAX_NODES_PER_BLOCK];  /* node ids in block (params) order */
+  int32_t adapt;                           /* AMWG/AMM: mmb_adapt (default :all) */
+  int32_t form;                            /* Slice: mmb_slice_form (default Multivariate) */
+  int32_t transform;                       /* Slice: transform flag (default false); AMWG/AMM/NUTS use true */
+  int32_t batchsize;                       /* AMWG batchsize (default 50) */
+  double target;                           /* AMWG target (0.44) / NUTS target (0.6) */
+  double beta;                             /* AMM beta (0.05) */
+  double scale;                            /* AMM scale (2.38) */
+  int32_t dim;                             /* unlisted block length (checked by mmb_create) */
+  int32_t ntuning;                         /* length of `tuning` */
+  const double* tuning;                    /* AMWG sigma[dim] | Slice width[dim] | AMM Sigma[dim*dim] col-major */
+} mmb_block_spec;
+
+typedef struct {
+  int32_t model;                           /* mmb_model_kind */
+  int32_t nblocks;
+  mmb_block_spec blocks[MMB_MAX_BLOCKS];   /* Model.samplers, in sweep order */
+  int32_t nobs;                            /* logistic: N (rows of X) */
+  int32_t ncoef;                           /* logistic: p (columns of X) */
+  double prior_sd;                         /* logistic: beta ~ MvNormal(p, prior_sd) */
+  int32_t reserved[8];
+} mmb_model_spec;
+
+/* Arguments of one mcmc window (mcmc.jl:36-83). */
+typedef struct {
+  int64_t iters;        /* window = iter+1 : iter+iters  (mcmc_master! `window`) */
+  int64_t burnin;       /* keep iteration i iff i > burnin && (i-burnin) % thin == 0 (mcmc.jl:76) */
+  int64_t thin;
+  int64_t model_burnin; /* Model.burnin: gate for adapt=:burnin (amwg.jl:55) and NUTS (nuts.jl:52) */
+  double* draws;        /* host out, Mamba Chains order n_kept x p_mon x K (iteration fastest) or NULL */
+  int32_t keep_device;  /* nonzero: keep this window's draws on the device (mmb_get_draws / GR) */
+  int32_t time_kernels; /* nonzero: bracket each kernel launch with HIP events (mmb_kernel_time) */
+} mmb_run_args;
+
+typedef struct mmb_engine mmb_engine;
+
+/* Engine lifetime ---------------------------------------------------------------- */
+int mmb_abi_version(void);
+int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out);
+void mmb_destroy(mmb_engine* e);
+const char* mmb_last_error(const mmb_engine* e); /* e may be NULL: last global error */
+
+/* setinputs! (initialization.jl:30-40): named data arrays.
+ * line: "x"(5), "y"(5); rats: "y"(150, rat-major), "x"(5); logistic: "X"(N*p row-major), "y"(N) */
+int mmb_set_data(mmb_engine* e, const char* name, const double* x, int64_t n);
+
+/* setinits! (initialization.jl:20-28): K chains, `init` is K x P row-major (chain-major),
+ * P = mmb_num_values(); global chain ids are chain_offset .. chain_offset+K-1 (they key the
+ * Philox streams, so a chain's trajectory does not depend on how chains are sharded). */
+int mmb_num_values(const mmb_engine* e);
+int mmb_num_monitored(const mmb_engine* e);
+int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_offset, uint64_t seed);
+
+/* mcmc_worker! loop for all chains of this engine (mcmc.jl:62-83). */
+int mmb_run(mmb_engine* e, const mmb_run_args* args);
+int64_t mmb_iter(const mmb_engine* e);              /* Model.iter after the last window */
+
+/* ModelState / gettune / settune! (mcmc.jl:56,82; simulation.jl:3-28):
+ * values: K x P row-major.  tune: K x mmb_tune_len() doubles in the canonical layout
+ * (DESIGN.md §tune layout; ints stored exactly as doubles). */
+int mmb_get_values(mmb_engine* e, double* values);
+int mmb_set_values(mmb_engine* e, const double* values);
+int64_t mmb_tune_len(const mmb_engine* e);
+int mmb_get_tune(mmb_engine* e, double* tune);
+int mmb_set_tune(mmb_engine* e, const double* tune);
+
+/* Draws of the last window kept on device (keep_device=1), host copy in Mamba order. */
+int64_t mmb_num_kept(const mmb_engine* e);
+int mmb_get_draws(mmb_engine* e, double* draws);
+
+/* Gelman-Rubin sufficient statistics of the device-kept draws (gelmandiag.jl:3-60).
+ * mmb_gr_range: per monitored param [min, max] over local chains/draws (for link()).
+ * mmb_gr_partials: per-chain mean/covariance reduced over local chains, after optional
+ * log/logit link (link_kind per param: 0 none, 1 log, 2 logit) and shift `shift[p]`;
+ * out has mmb_gr_len() doubles: these are summed across GPUs (RCCL all-reduce). */
+int mmb_gr_range(mmb_engine* e, double* minmax /* 2*p */);
+int64_t mmb_gr_len(const mmb_engine* e);
+int mmb_gr_partials(mmb_engine* e, const int32_t* link_kind, const double* shift, double* out);
+
+/* Timing / sync (bench.py roofline) */
+int mmb_sync(mmb_engine* e);
+int mmb_kernel_time(const mmb_engine* e, double* total_ms, int64_t* launches, int64_t* units);
+int mmb_state_bytes(const mmb_engine* e, double* bytes_per_chain_update);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAMBA_HIP_H */

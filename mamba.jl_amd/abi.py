@@ -1,0 +1,110 @@
+"""ctypes mirror of include/mamba_hip.h and the loader of libmambahip.so.
+
+The product path is the HIP engine only: if the shared library is missing (not
+built, or built without a GPU-capable runtime) every entry point raises
+RuntimeError -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+MMB_MAX_BLOCKS = 8
+MMB_MAX_NODES_PER_BLOCK = 4
+
+MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = 1, 2, 3
+MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
+MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
+MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
+MMB_LINE_BETA, MMB_LINE_S2 = 0, 1
+(MMB_RATS_S2_C, MMB_RATS_ALPHA, MMB_RATS_MU_ALPHA, MMB_RATS_S2_ALPHA, MMB_RATS_BETA, MMB_RATS_MU_BETA,
+ MMB_RATS_S2_BETA) = range(7)
+MMB_LOGISTIC_BETA = 0
+
+ERRORS = {-1: "invalid argument", -2: "unsupported model/scheme", -3: "HIP runtime error",
+          -4: "call out of order", -5: "out of memory"}
+
+
+class BlockSpec(C.Structure):
+    _fields_ = [("sampler", C.c_int32), ("nnodes", C.c_int32),
+                ("nodes", C.c_int32 * MMB_MAX_NODES_PER_BLOCK), ("adapt", C.c_int32),
+                ("form", C.c_int32), ("transform", C.c_int32), ("batchsize", C.c_int32),
+                ("target", C.c_double), ("beta", C.c_double), ("scale", C.c_double),
+                ("dim", C.c_int32), ("ntuning", C.c_int32), ("tuning", C.POINTER(C.c_double))]
+
+
+class ModelSpec(C.Structure):
+    _fields_ = [("model", C.c_int32), ("nblocks", C.c_int32),
+                ("blocks", BlockSpec * MMB_MAX_BLOCKS), ("nobs", C.c_int32), ("ncoef", C.c_int32),
+                ("prior_sd", C.c_double), ("reserved", C.c_int32 * 8)]
+
+
+class RunArgs(C.Structure):
+    _fields_ = [("iters", C.c_int64), ("burnin", C.c_int64), ("thin", C.c_int64),
+                ("model_burnin", C.c_int64), ("draws", C.POINTER(C.c_double)),
+                ("keep_device", C.c_int32), ("time_kernels", C.c_int32)]
+
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmambahip.so")
+_lib = None
+
+
+def _declare(lib):
+    P, D, I64, I32 = C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32
+    sig = {
+        "mmb_abi_version": (C.c_int, []),
+        "mmb_create": (C.c_int, [C.POINTER(ModelSpec), C.c_int, C.POINTER(C.c_void_p)]),
+        "mmb_destroy": (None, [P]),
+        "mmb_last_error": (C.c_char_p, [P]),
+        "mmb_set_data": (C.c_int, [P, C.c_char_p, D, I64]),
+        "mmb_num_values": (C.c_int, [P]),
+        "mmb_num_monitored": (C.c_int, [P]),
+        "mmb_init_chains": (C.c_int, [P, D, I64, I64, C.c_uint64]),
+        "mmb_run": (C.c_int, [P, C.POINTER(RunArgs)]),
+        "mmb_iter": (I64, [P]),
+        "mmb_get_values": (C.c_int, [P, D]),
+        "mmb_set_values": (C.c_int, [P, D]),
+        "mmb_tune_len": (I64, [P]),
+        "mmb_get_tune": (C.c_int, [P, D]),
+        "mmb_set_tune": (C.c_int, [P, D]),
+        "mmb_num_kept": (I64, [P]),
+        "mmb_get_draws": (C.c_int, [P, D]),
+        "mmb_gr_range": (C.c_int, [P, D]),
+        "mmb_gr_len": (I64, [P]),
+        "mmb_gr_partials": (C.c_int, [P, C.POINTER(I32), D, D]),
+        "mmb_sync": (C.c_int, [P]),
+        "mmb_kernel_time": (C.c_int, [P, D, C.POINTER(I64), C.POINTER(I64)]),
+        "mmb_state_bytes": (C.c_int, [P, D]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def lib():
+    """Load libmambahip.so (the HIP engine).  Raises if it is missing: no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        try:  # pin the HIP runtime torch ships, if torch is present (single runtime per process)
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        _lib = _declare(C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL))
+        if _lib.mmb_abi_version() != 1:
+            raise RuntimeError("libmambahip.so ABI version mismatch")
+    return _lib
+
+
+def check(rc, eng=None):
+    if rc != 0:
+        msg = lib().mmb_last_error(eng)
+        raise RuntimeError(f"mamba_hip error {rc} ({ERRORS.get(rc, '?')}): "
+                           f"{msg.decode() if msg else ''}")
+    return rc
+
+
+def dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))

@@ -1,0 +1,136 @@
+// device.h — shared device-side definitions for the sweep kernels.
+//
+// Execution model: one chain is advanced by a *group* of G
+// lanes of a wave64 (G = 32 for rats: lane i <-> rat i / block element i, two
+// chains per wave; G = 1 for line: one chain per lane).  Element e of a block's
+// unlisted vector lives in lane e % G, register slot e / G (R slots per lane).
+// Group-uniform control flow only; group reductions are xor-butterflies inside
+// the G-aligned lane group, so every lane of a group ends with the same value.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mamba_hip.h"
+#include "mmb_math.h"
+
+#define MMB_MAXB MMB_MAX_BLOCKS
+
+// Per-block descriptor passed in kernel arguments (constant memory, uniform access).
+struct DBlock {
+  int32_t kind, nn, d, transform, form, adapt, batchsize, sigl_diag;
+  int32_t nodes[4];
+  int32_t emap[4];       // line/rats scalar blocks: element -> value index / node id
+  double target, beta, scale;
+  double width0;         // Slice: scalar width
+  const double* width;   // Slice: widths[d] (device) or null when scalar
+  const double* sigl;    // AMM: chol(Sigma) lower, row-major d x d (device)
+  // tune state (device, chain-major)
+  double* t_sigma;       // AMWG  [K][DP]
+  double* t_accept;      // AMWG  [K][DP]
+  int32_t* t_m;          // AMWG/AMM/NUTS m [K]
+  int32_t* t_flags;      // [K] bit0 adapt, bit1 AMM alias, bit2 AMM factor valid, bit3 NUTS init
+  double* t_Mv;          // AMM   [K][DP]
+  double* t_Mvv;         // AMM   [K][TP] packed lower, row-major (slot(i,k) = i(i+1)/2 + k)
+  double* t_Ls;          // AMM   [K][TP] factor, in-place slot storage
+  uint8_t* t_piv;        // AMM   [K][DP] pivot order
+  double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
+};
+
+struct SweepArgs {
+  int32_t K;             // chains in this shard
+  uint32_t chain_offset; // global id of chain 0
+  uint64_t seed;
+  int64_t iter0;         // window starts at iter0+1
+  int32_t n_iters;
+  int32_t nb;
+  int64_t burnin, thin, model_burnin;
+  int64_t kept_base;     // kept rows before this launch (within the mmb_run window)
+  int64_t kept_origin;   // kept count at the window start (rows are relative to the window)
+  double* vals;          // model-specific device layout
+  double* draws;         // [n_kept][pmon][K] or null
+  const double* data0;   // model data (rats: y[150]; line: x[5], y[5] packed as 10)
+  double ig_c;           // 0.001 log(0.001) - lgamma(0.001)
+  double xbar;           // rats
+  double xm[5];          // rats: x - xbar
+  double lx[5], ly[5];   // line data
+  const DBlock* blocks;  // device array [nb] (uniform, scalar-cache loads)
+};
+
+MMB_HD int mmb_tri(int i) { return (i * (i + 1)) >> 1; }
+MMB_HD int mmb_slot(int i, int k) { return i >= k ? mmb_tri(i) + k : mmb_tri(k) + i; }
+
+// wave-scope compiler/memory ordering between a lane's LDS write and another lane's read
+__device__ __forceinline__ void grp_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int G>
+struct Grp {
+  int lane;
+  __device__ __forceinline__ Grp() : lane((int)(threadIdx.x & (G - 1))) {}
+  __device__ __forceinline__ double sum(double x) const {
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+  }
+  __device__ __forceinline__ void sum2(double& x, double& y) const {
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) {
+      double a = __shfl_xor(x, m, 64);
+      double b = __shfl_xor(y, m, 64);
+      x += a;
+      y += b;
+    }
+  }
+  __device__ __forceinline__ double bcast(double x, int src) const {
+    if (G == 1) return x;
+    int base = (int)(threadIdx.x & 63) & ~(G - 1);
+    return __shfl(x, base + src, 64);
+  }
+  __device__ __forceinline__ int bcast_i(int x, int src) const {
+    if (G == 1) return x;
+    int base = (int)(threadIdx.x & 63) & ~(G - 1);
+    return __shfl(x, base + src, 64);
+  }
+  // Lexicographic (key desc, pos asc) argmax; carries value and index.
+  __device__ __forceinline__ void argmax(double& key, int& pos, double& val, int& idx) const {
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) {
+      double ok = __shfl_xor(key, m, 64);
+      int op = __shfl_xor(pos, m, 64);
+      double ov = __shfl_xor(val, m, 64);
+      int oi = __shfl_xor(idx, m, 64);
+      bool take = (ok > key) || (ok == key && op < pos);
+      if (take) { key = ok; pos = op; val = ov; idx = oi; }
+    }
+  }
+};
+
+// Julia min(a, b): NaN propagates
+__device__ __forceinline__ double jmin(double a, double b) {
+  if (isnan(a)) return a;
+  if (isnan(b)) return b;
+  return b < a ? b : a;
+}
+
+// StatsFuns normlogpdf(mu, sig, x) with insupport(Normal, x)
+__device__ __forceinline__ double d_normlogpdf(double mu, double sig, double logsig, double x) {
+  if (isnan(x)) return -__builtin_inf();
+  double z = (x - mu) / sig;
+  return -(z * z + MMB_LOG2PI) / 2.0 - logsig;
+}
+// InverseGamma(0.001, 0.001) with insupport 0 <= x <= Inf, + log(x) Jacobian when transformed
+__device__ __forceinline__ double d_iglogpdf(double igc, double x, int transform) {
+  if (!(0.0 <= x && x <= __builtin_inf())) return -__builtin_inf();
+  double lx = mmb_log(x);
+  double lp = igc - (0.001 + 1.0) * lx - 0.001 / x;
+  return transform ? lp + lx : lp;
+}
+// IsoNormal via PDMats ScalMat: -0.5*(k*log2pi + k*log(sig^2) + ssq/sig^2)
+__device__ __forceinline__ double d_iso(int k, double sig, double ssq) {
+  double value = sig * sig;
+  double invv = 1.0 / value;
+  return -0.5 * ((k * MMB_LOG2PI + k * mmb_log(value)) + ssq * invv);
+}

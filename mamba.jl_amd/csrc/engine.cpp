@@ -1,0 +1,758 @@
+// engine.cpp — host side of libmambahip.so: the C ABI of include/mamba_hip.h.
+//
+// mmb_run is mcmc_master!/mcmc_worker! (src/model/mcmc.jl:36-83) for every chain of
+// this engine's shard: it launches the fused sweep kernel over windows of iterations
+// on the engine's stream and copies the kept draws out in Mamba's Chains order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device.h"
+#include "models.h"
+
+hipError_t mmb_launch_sweep(int model, const SweepArgs& A, hipStream_t st);
+hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
+                               hipStream_t st);
+hipError_t mmb_launch_gr_stats(int pmon, int64_t n, int K, const double* draws, const int32_t* link,
+                               const double* shift, double* stats, hipStream_t st);
+
+static thread_local std::string g_last_error;
+
+struct BlockHost {
+  mmb_block_spec spec;
+  std::vector<double> tuning;
+  int d = 0, T = 0, tune_len = 0;
+  std::vector<double> sigl;  // AMM chol(Sigma) lower row-major
+  bool sigl_diag = false;
+  // device
+  double *sigma = nullptr, *accept = nullptr, *Mv = nullptr, *Mvv = nullptr, *Ls = nullptr;
+  double *nuts = nullptr, *width = nullptr, *sigl_d = nullptr;
+  int32_t *m = nullptr, *flags = nullptr;
+  uint8_t* piv = nullptr;
+};
+
+struct mmb_engine {
+  mmb_model_spec spec{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int model = 0;
+  int P = 0, pmon = 0, VS = 0, DP = 0, TP = 0;
+  std::vector<BlockHost> blocks;
+  // data
+  std::vector<double> x, y, X;
+  bool have_data = false;
+  double* d_data = nullptr;
+  // chains
+  int64_t K = 0, chain_offset = 0;
+  uint64_t seed = 0;
+  int64_t iter = 0;
+  double* d_vals = nullptr;
+  DBlock* d_blocks = nullptr;
+  // draws of the last window
+  double* d_draws = nullptr;
+  size_t draws_cap = 0;
+  int64_t n_kept = 0;
+  // timing
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double kernel_ms = 0.0;
+  int64_t launches = 0, units = 0;
+  std::string err;
+};
+
+static int fail(mmb_engine* e, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  if (e) e->err = buf;
+  return code;
+}
+
+#define HIPCHK(e, call)                                                                  \
+  do {                                                                                   \
+    hipError_t _st = (call);                                                             \
+    if (_st != hipSuccess)                                                               \
+      return fail((e), MMB_E_HIP, "%s failed: %s", #call, hipGetErrorString(_st));       \
+  } while (0)
+
+static int node_dim(const mmb_model_spec& s, int node, bool* positive) {
+  bool pos = false;
+  int d = -1;
+  if (s.model == MMB_MODEL_LINE) {
+    if (node == MMB_LINE_BETA) d = 2;
+    else if (node == MMB_LINE_S2) { d = 1; pos = true; }
+  } else if (s.model == MMB_MODEL_RATS) {
+    static const int dims[7] = {1, 30, 1, 1, 30, 1, 1};
+    static const int posv[7] = {1, 0, 0, 1, 0, 0, 1};
+    if (node >= 0 && node < 7) { d = dims[node]; pos = posv[node]; }
+  } else if (s.model == MMB_MODEL_LOGISTIC) {
+    if (node == MMB_LOGISTIC_BETA) d = s.ncoef;
+  }
+  if (positive) *positive = pos;
+  return d;
+}
+
+static int tri(int i) { return i * (i + 1) / 2; }
+
+static int tune_len_of(int kind, int d) {
+  switch (kind) {
+    case MMB_SAMPLER_AMWG: return 2 + 2 * d;
+    case MMB_SAMPLER_AMM: return 4 + 2 * d + 2 * tri(d);
+    case MMB_SAMPLER_NUTS: return 9;
+    default: return 0;
+  }
+}
+
+static int chol_lower(int d, const double* A, double* L) {  // A column-major
+  for (int i = 0; i < d * d; ++i) L[i] = 0.0;
+  for (int j = 0; j < d; ++j) {
+    double s = A[j * d + j];
+    for (int k = 0; k < j; ++k) s -= L[j * d + k] * L[j * d + k];
+    if (!(s > 0.0)) return -1;
+    double ljj = std::sqrt(s);
+    L[j * d + j] = ljj;
+    for (int i = j + 1; i < d; ++i) {
+      double t = A[j * d + i];
+      for (int k = 0; k < j; ++k) t -= L[i * d + k] * L[j * d + k];
+      L[i * d + j] = t / ljj;
+    }
+  }
+  return 0;
+}
+
+// C linkage comes from the extern "C" declarations in include/mamba_hip.h.
+
+int mmb_abi_version(void) { return MMB_ABI_VERSION; }
+
+const char* mmb_last_error(const mmb_engine* e) {
+  if (e && !e->err.empty()) return e->err.c_str();
+  return g_last_error.c_str();
+}
+
+int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
+  if (!spec || !out) return fail(nullptr, MMB_E_ARG, "null argument");
+  *out = nullptr;
+  if (spec->nblocks < 1 || spec->nblocks > MMB_MAX_BLOCKS)
+    return fail(nullptr, MMB_E_ARG, "nblocks must be in 1..%d", MMB_MAX_BLOCKS);
+  mmb_engine* e = new mmb_engine();
+  e->spec = *spec;
+  e->model = spec->model;
+  if (e->model == MMB_MODEL_RATS) {
+    e->P = 65; e->pmon = 3; e->VS = Mdl<MMB_MODEL_RATS>::VS;
+    e->DP = Mdl<MMB_MODEL_RATS>::DP; e->TP = Mdl<MMB_MODEL_RATS>::TP;
+  } else if (e->model == MMB_MODEL_LINE) {
+    e->P = 3; e->pmon = 3; e->VS = Mdl<MMB_MODEL_LINE>::VS;
+    e->DP = Mdl<MMB_MODEL_LINE>::DP; e->TP = Mdl<MMB_MODEL_LINE>::TP;
+  } else if (e->model == MMB_MODEL_LOGISTIC) {
+    delete e;
+    return fail(nullptr, MMB_E_UNSUPPORTED, "logistic model: NUTS engine not built in this version");
+  } else {
+    delete e;
+    return fail(nullptr, MMB_E_UNSUPPORTED, "unknown model kind %d", spec->model);
+  }
+  for (int b = 0; b < spec->nblocks; ++b) {
+    const mmb_block_spec& s = spec->blocks[b];
+    BlockHost h;
+    h.spec = s;
+    if (s.nnodes < 1 || s.nnodes > MMB_MAX_NODES_PER_BLOCK) {
+      delete e;
+      return fail(nullptr, MMB_E_ARG, "block %d: bad node count", b);
+    }
+    int d = 0, nvec = 0;
+    for (int a = 0; a < s.nnodes; ++a) {
+      for (int a2 = 0; a2 < a; ++a2)
+        if (s.nodes[a2] == s.nodes[a]) {
+          delete e;
+          return fail(nullptr, MMB_E_ARG, "block %d: repeated node", b);
+        }
+      int nd = node_dim(*spec, s.nodes[a], nullptr);
+      if (nd < 0) {
+        delete e;
+        return fail(nullptr, MMB_E_ARG, "block %d: node id %d invalid for model", b, s.nodes[a]);
+      }
+      if (nd > 1) nvec++;
+      d += nd;
+    }
+    if (s.dim != 0 && s.dim != d) {
+      delete e;
+      return fail(nullptr, MMB_E_ARG, "block %d: dim %d != unlisted length %d", b, s.dim, d);
+    }
+    h.d = d;
+    h.T = tri(d);
+    if (e->model == MMB_MODEL_RATS && nvec > 0 && (s.nnodes != 1)) {
+      delete e;
+      return fail(nullptr, MMB_E_UNSUPPORTED, "rats: alpha/beta must form their own block");
+    }
+    if (s.ntuning > 0) h.tuning.assign(s.tuning, s.tuning + s.ntuning);
+    switch (s.sampler) {
+      case MMB_SAMPLER_AMWG:
+        if (!(s.ntuning == 1 || s.ntuning == d)) {
+          delete e;
+          return fail(nullptr, MMB_E_ARG, "length(sigma) differs from variate length %d", d);
+        }
+        if (s.batchsize <= 0) { delete e; return fail(nullptr, MMB_E_ARG, "batchsize must be positive"); }
+        break;
+      case MMB_SAMPLER_AMM: {
+        if (s.ntuning != d * d) {
+          delete e;
+          return fail(nullptr, MMB_E_ARG, "Sigma dimension differs from variate length %d", d);
+        }
+        h.sigl.resize((size_t)d * d);
+        if (chol_lower(d, s.tuning, h.sigl.data())) {
+          delete e;
+          return fail(nullptr, MMB_E_ARG, "AMM Sigma is not positive definite");
+        }
+        h.sigl_diag = true;
+        for (int i = 0; i < d; ++i)
+          for (int k = 0; k < i; ++k)
+            if (h.sigl[i * d + k] != 0.0) h.sigl_diag = false;
+        break;
+      }
+      case MMB_SAMPLER_SLICE:
+        if (!(s.ntuning == 1 || s.ntuning == d)) {
+          delete e;
+          return fail(nullptr, MMB_E_ARG, "length(width) differs from variate length %d", d);
+        }
+        break;
+      case MMB_SAMPLER_GIBBS:
+        if (s.nnodes != 1) {
+          delete e;
+          return fail(nullptr, MMB_E_UNSUPPORTED, "Gibbs: one node per block");
+        }
+        break;
+      case MMB_SAMPLER_NUTS:
+        delete e;
+        return fail(nullptr, MMB_E_UNSUPPORTED, "NUTS for this model is not lowered in this version");
+      default:
+        delete e;
+        return fail(nullptr, MMB_E_ARG, "unknown sampler kind %d", s.sampler);
+    }
+    h.tune_len = tune_len_of(s.sampler, d);
+    e->blocks.push_back(h);
+  }
+  hipError_t st = hipSetDevice(device);
+  if (st != hipSuccess) {
+    delete e;
+    return fail(nullptr, MMB_E_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(st));
+  }
+  e->device = device;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+    delete e;
+    return fail(nullptr, MMB_E_HIP, "stream/event creation failed");
+  }
+  *out = e;
+  return 0;
+}
+
+static void free_dev(mmb_engine* e) {
+  for (auto& h : e->blocks) {
+    void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.width, h.sigl_d, h.m, h.flags, h.piv};
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+    h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.width = h.sigl_d = nullptr;
+    h.m = h.flags = nullptr;
+    h.piv = nullptr;
+  }
+  if (e->d_vals) (void)hipFree(e->d_vals);
+  if (e->d_blocks) (void)hipFree(e->d_blocks);
+  if (e->d_draws) (void)hipFree(e->d_draws);
+  e->d_vals = nullptr;
+  e->d_blocks = nullptr;
+  e->d_draws = nullptr;
+  e->draws_cap = 0;
+}
+
+void mmb_destroy(mmb_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  free_dev(e);
+  if (e->d_data) (void)hipFree(e->d_data);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int mmb_set_data(mmb_engine* e, const char* name, const double* x, int64_t n) {
+  if (!e || !name || !x) return fail(e, MMB_E_ARG, "null argument");
+  std::string nm(name);
+  if (e->model == MMB_MODEL_LINE) {
+    if (n != 5) return fail(e, MMB_E_ARG, "line: %s must have 5 elements", name);
+    if (nm == "x") e->x.assign(x, x + 5);
+    else if (nm == "y") e->y.assign(x, x + 5);
+    else return fail(e, MMB_E_ARG, "line: unknown input %s", name);
+  } else if (e->model == MMB_MODEL_RATS) {
+    if (nm == "y") {
+      if (n != 150) return fail(e, MMB_E_ARG, "rats: y must have 150 elements");
+      e->y.assign(x, x + 150);
+    } else if (nm == "x") {
+      if (n != 5) return fail(e, MMB_E_ARG, "rats: x must have 5 elements");
+      e->x.assign(x, x + 5);
+    } else {
+      return fail(e, MMB_E_ARG, "rats: unknown input %s", name);
+    }
+  }
+  e->have_data = !e->x.empty() && !e->y.empty();
+  if (e->have_data && e->model == MMB_MODEL_RATS) {
+    HIPCHK(e, hipSetDevice(e->device));
+    if (!e->d_data) HIPCHK(e, hipMalloc(&e->d_data, 150 * sizeof(double)));
+    HIPCHK(e, hipMemcpy(e->d_data, e->y.data(), 150 * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int mmb_num_values(const mmb_engine* e) { return e ? e->P : MMB_E_ARG; }
+int mmb_num_monitored(const mmb_engine* e) { return e ? e->pmon : MMB_E_ARG; }
+int64_t mmb_iter(const mmb_engine* e) { return e ? e->iter : MMB_E_ARG; }
+int64_t mmb_num_kept(const mmb_engine* e) { return e ? e->n_kept : MMB_E_ARG; }
+
+int64_t mmb_tune_len(const mmb_engine* e) {
+  if (!e) return MMB_E_ARG;
+  int64_t n = 0;
+  for (auto& h : e->blocks) n += h.tune_len;
+  return n;
+}
+
+// canonical values (K x P) <-> device layout
+static void to_device_layout(const mmb_engine* e, const double* v, double* dv) {
+  if (e->model == MMB_MODEL_RATS) {
+    std::fill(dv, dv + e->VS, 0.0);
+    for (int i = 0; i < 30; ++i) { dv[i] = v[1 + i]; dv[32 + i] = v[33 + i]; }
+    dv[64] = v[0]; dv[65] = v[31]; dv[66] = v[32]; dv[67] = v[63]; dv[68] = v[64];
+  } else {
+    dv[0] = v[0]; dv[1] = v[1]; dv[2] = v[2]; dv[3] = 0.0;
+  }
+}
+static void from_device_layout(const mmb_engine* e, const double* dv, double* v) {
+  if (e->model == MMB_MODEL_RATS) {
+    for (int i = 0; i < 30; ++i) { v[1 + i] = dv[i]; v[33 + i] = dv[32 + i]; }
+    v[0] = dv[64]; v[31] = dv[65]; v[32] = dv[66]; v[63] = dv[67]; v[64] = dv[68];
+  } else {
+    v[0] = dv[0]; v[1] = dv[1]; v[2] = dv[2];
+  }
+}
+
+int mmb_set_values(mmb_engine* e, const double* values) {
+  if (!e || !values) return fail(e, MMB_E_ARG, "null argument");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  std::vector<double> h((size_t)e->K * e->VS);
+  for (int64_t k = 0; k < e->K; ++k) to_device_layout(e, values + k * e->P, h.data() + k * e->VS);
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipMemcpy(e->d_vals, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mmb_get_values(mmb_engine* e, double* values) {
+  if (!e || !values) return fail(e, MMB_E_ARG, "null argument");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  std::vector<double> h((size_t)e->K * e->VS);
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipMemcpy(h.data(), e->d_vals, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  for (int64_t k = 0; k < e->K; ++k) from_device_layout(e, h.data() + k * e->VS, values + k * e->P);
+  return 0;
+}
+
+static int upload_blocks(mmb_engine* e) {
+  std::vector<DBlock> db(e->blocks.size());
+  for (size_t b = 0; b < e->blocks.size(); ++b) {
+    BlockHost& h = e->blocks[b];
+    DBlock& d = db[b];
+    std::memset(&d, 0, sizeof d);
+    d.kind = h.spec.sampler;
+    d.nn = h.spec.nnodes;
+    d.d = h.d;
+    d.transform = h.spec.sampler == MMB_SAMPLER_SLICE ? h.spec.transform : 1;
+    d.form = h.spec.form;
+    d.adapt = h.spec.adapt;
+    d.batchsize = h.spec.batchsize;
+    d.sigl_diag = h.sigl_diag;
+    for (int a = 0; a < 4; ++a) d.nodes[a] = a < h.spec.nnodes ? h.spec.nodes[a] : -1;
+    // line: element -> value index (beta -> 0,1; s2 -> 2)
+    int o = 0;
+    for (int a = 0; a < h.spec.nnodes && o < 4; ++a) {
+      int n = h.spec.nodes[a];
+      if (e->model == MMB_MODEL_LINE) {
+        if (n == MMB_LINE_BETA) { d.emap[o++] = 0; if (o < 4) d.emap[o++] = 1; }
+        else d.emap[o++] = 2;
+      } else {
+        d.emap[o++] = n;
+      }
+    }
+    d.target = h.spec.target;
+    d.beta = h.spec.beta;
+    d.scale = h.spec.scale;
+    d.width0 = h.tuning.empty() ? 0.0 : h.tuning[0];
+    d.width = (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) ? h.width : nullptr;
+    d.sigl = h.sigl_d;
+    d.t_sigma = h.sigma; d.t_accept = h.accept; d.t_m = h.m; d.t_flags = h.flags;
+    d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_nuts = h.nuts;
+  }
+  if (!e->d_blocks) HIPCHK(e, hipMalloc(&e->d_blocks, MMB_MAX_BLOCKS * sizeof(DBlock)));
+  HIPCHK(e, hipMemcpy(e->d_blocks, db.data(), db.size() * sizeof(DBlock), hipMemcpyHostToDevice));
+  return 0;
+}
+
+template <class T>
+static hipError_t dalloc(T** p, size_t n) {
+  return hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_offset, uint64_t seed) {
+  if (!e || !init) return fail(e, MMB_E_ARG, "null argument");
+  if (K < 1 || K > (int64_t)1 << 30) return fail(e, MMB_E_ARG, "K out of range");
+  if (chain_offset < 0 || chain_offset + K > ((int64_t)1 << 32))
+    return fail(e, MMB_E_ARG, "global chain ids must fit in 32 bits");
+  if (!e->have_data) return fail(e, MMB_E_STATE, "inputs must be set before inits");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  free_dev(e);
+  e->K = K;
+  e->chain_offset = chain_offset;
+  e->seed = seed;
+  e->iter = 0;
+  e->n_kept = 0;
+  HIPCHK(e, dalloc(&e->d_vals, (size_t)K * e->VS));
+  const size_t DP = e->DP, TP = e->TP;
+  for (auto& h : e->blocks) {
+    HIPCHK(e, dalloc(&h.m, K));
+    HIPCHK(e, dalloc(&h.flags, K));
+    HIPCHK(e, hipMemset(h.m, 0, K * sizeof(int32_t)));
+    HIPCHK(e, hipMemset(h.flags, 0, K * sizeof(int32_t)));
+    if (h.spec.sampler == MMB_SAMPLER_AMWG) {
+      HIPCHK(e, dalloc(&h.sigma, K * DP));
+      HIPCHK(e, dalloc(&h.accept, K * DP));
+      std::vector<double> sg(K * DP, 0.0);
+      for (int64_t k = 0; k < K; ++k)
+        for (int i = 0; i < h.d; ++i) sg[k * DP + i] = h.tuning.size() == 1 ? h.tuning[0] : h.tuning[i];
+      HIPCHK(e, hipMemcpy(h.sigma, sg.data(), sg.size() * sizeof(double), hipMemcpyHostToDevice));
+      HIPCHK(e, hipMemset(h.accept, 0, K * DP * sizeof(double)));
+    } else if (h.spec.sampler == MMB_SAMPLER_AMM) {
+      HIPCHK(e, dalloc(&h.Mv, K * DP));
+      HIPCHK(e, dalloc(&h.Mvv, K * TP));
+      HIPCHK(e, dalloc(&h.Ls, K * TP));
+      HIPCHK(e, dalloc(&h.piv, K * DP));
+      HIPCHK(e, hipMemset(h.Mv, 0, K * DP * sizeof(double)));
+      HIPCHK(e, hipMemset(h.Mvv, 0, K * TP * sizeof(double)));
+      HIPCHK(e, hipMemset(h.Ls, 0, K * TP * sizeof(double)));
+      std::vector<uint8_t> pv(K * DP);
+      for (int64_t k = 0; k < K; ++k)
+        for (size_t i = 0; i < DP; ++i) pv[k * DP + i] = (uint8_t)i;
+      HIPCHK(e, hipMemcpy(h.piv, pv.data(), pv.size(), hipMemcpyHostToDevice));
+      HIPCHK(e, dalloc(&h.sigl_d, (size_t)h.d * h.d));
+      HIPCHK(e, hipMemcpy(h.sigl_d, h.sigl.data(), h.sigl.size() * sizeof(double), hipMemcpyHostToDevice));
+    } else if (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) {
+      HIPCHK(e, dalloc(&h.width, h.tuning.size()));
+      HIPCHK(e, hipMemcpy(h.width, h.tuning.data(), h.tuning.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+  }
+  int rc = upload_blocks(e);
+  if (rc) return rc;
+  return mmb_set_values(e, init);
+}
+
+static int64_t kept_upto(int64_t t, int64_t burnin, int64_t thin) {
+  return t > burnin ? (t - burnin) / thin : 0;
+}
+
+static void fill_args(const mmb_engine* e, SweepArgs& A) {
+  std::memset(&A, 0, sizeof A);
+  A.K = (int32_t)e->K;
+  A.chain_offset = (uint32_t)e->chain_offset;
+  A.seed = e->seed;
+  A.nb = (int32_t)e->blocks.size();
+  A.vals = e->d_vals;
+  A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
+  A.blocks = e->d_blocks;
+  if (e->model == MMB_MODEL_RATS) {
+    double s = 0.0;
+    for (int i = 0; i < 5; ++i) s += e->x[i];
+    A.xbar = s / 5.0;
+    for (int i = 0; i < 5; ++i) A.xm[i] = e->x[i] - A.xbar;
+    A.data0 = e->d_data;
+  } else {
+    for (int i = 0; i < 5; ++i) { A.lx[i] = e->x[i]; A.ly[i] = e->y[i]; }
+  }
+}
+
+static int iters_per_launch(const mmb_engine* e) {
+  const char* s = std::getenv("MMB_ITERS_PER_LAUNCH");
+  if (s && std::atoi(s) > 0) return std::atoi(s);
+  return e->model == MMB_MODEL_RATS ? 8 : 64;
+}
+
+int mmb_run(mmb_engine* e, const mmb_run_args* a) {
+  if (!e || !a) return fail(e, MMB_E_ARG, "null argument");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  if (a->iters < 0 || a->thin < 1 || a->burnin < 0)
+    return fail(e, MMB_E_ARG, "iters >= 0, thin >= 1, burnin >= 0 required");
+  if (e->iter + a->iters > 0xffffffffLL) return fail(e, MMB_E_ARG, "iteration counter overflow");
+  HIPCHK(e, hipSetDevice(e->device));
+  const int64_t it0 = e->iter;
+  const int64_t kept0 = kept_upto(it0, a->burnin, a->thin);
+  const int64_t nk = kept_upto(it0 + a->iters, a->burnin, a->thin) - kept0;
+  const bool want = (a->draws != nullptr) || a->keep_device;
+  if (want && nk > 0) {
+    size_t need = (size_t)nk * e->pmon * e->K;
+    if (need > e->draws_cap) {
+      if (e->d_draws) HIPCHK(e, hipFree(e->d_draws));
+      e->d_draws = nullptr;
+      HIPCHK(e, dalloc(&e->d_draws, need));
+      e->draws_cap = need;
+    }
+  }
+  SweepArgs A;
+  fill_args(e, A);
+  A.burnin = a->burnin;
+  A.thin = a->thin;
+  A.model_burnin = a->model_burnin;
+  A.kept_origin = kept0;
+  A.draws = (want && nk > 0) ? e->d_draws : nullptr;
+  const int W = iters_per_launch(e);
+  e->kernel_ms = 0.0;
+  e->launches = 0;
+  e->units = 0;
+  for (int64_t done = 0; done < a->iters; done += W) {
+    int w = (int)std::min<int64_t>(W, a->iters - done);
+    A.iter0 = it0 + done;
+    A.n_iters = w;
+    if (a->time_kernels) HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    hipError_t st = mmb_launch_sweep(e->model, A, e->stream);
+    if (st != hipSuccess) return fail(e, MMB_E_HIP, "sweep launch: %s", hipGetErrorString(st));
+    if (a->time_kernels) {
+      HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+      HIPCHK(e, hipEventSynchronize(e->ev1));
+      float ms = 0.f;
+      HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+      e->kernel_ms += ms;
+    }
+    e->launches += 1;
+    e->units += (int64_t)w * e->K;
+  }
+  e->iter = it0 + a->iters;
+  e->n_kept = want ? nk : 0;
+  if (a->draws && nk > 0) {
+    std::vector<double> h((size_t)nk * e->pmon * e->K);
+    HIPCHK(e, hipMemcpyAsync(h.data(), e->d_draws, h.size() * sizeof(double), hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    // Mamba Chains value: n x p x m, column-major (iteration fastest)
+    for (int64_t i = 0; i < nk; ++i)
+      for (int j = 0; j < e->pmon; ++j)
+        for (int64_t k = 0; k < e->K; ++k)
+          a->draws[i + nk * (j + (int64_t)e->pmon * k)] = h[(i * e->pmon + j) * e->K + k];
+  }
+  return 0;
+}
+
+int mmb_get_draws(mmb_engine* e, double* draws) {
+  if (!e || !draws) return fail(e, MMB_E_ARG, "null argument");
+  const int64_t nk = e->n_kept;
+  if (nk == 0) return 0;
+  std::vector<double> h((size_t)nk * e->pmon * e->K);
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipMemcpy(h.data(), e->d_draws, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < nk; ++i)
+    for (int j = 0; j < e->pmon; ++j)
+      for (int64_t k = 0; k < e->K; ++k)
+        draws[i + nk * (j + (int64_t)e->pmon * k)] = h[(i * e->pmon + j) * e->K + k];
+  return 0;
+}
+
+// ---------------------------------------------------------------- tune (canonical layout)
+template <class T>
+static int d2h(mmb_engine* e, std::vector<T>& h, const T* d, size_t n) {
+  h.resize(n);
+  HIPCHK(e, hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
+  return 0;
+}
+template <class T>
+static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
+  HIPCHK(e, hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mmb_get_tune(mmb_engine* e, double* tune) {
+  if (!e || !tune) return fail(e, MMB_E_ARG, "null argument");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  const int64_t TL = mmb_tune_len(e), K = e->K;
+  const size_t DP = e->DP, TP = e->TP;
+  int64_t off = 0;
+  for (auto& h : e->blocks) {
+    std::vector<int32_t> m, fl;
+    int rc;
+    if ((rc = d2h(e, m, h.m, K)) || (rc = d2h(e, fl, h.flags, K))) return rc;
+    if (h.spec.sampler == MMB_SAMPLER_AMWG) {
+      std::vector<double> sg, ac;
+      if ((rc = d2h(e, sg, h.sigma, K * DP)) || (rc = d2h(e, ac, h.accept, K * DP))) return rc;
+      for (int64_t k = 0; k < K; ++k) {
+        double* t = tune + k * TL + off;
+        t[0] = (fl[k] & 1) ? 1.0 : 0.0;
+        t[1] = m[k];
+        for (int i = 0; i < h.d; ++i) { t[2 + i] = sg[k * DP + i]; t[2 + h.d + i] = ac[k * DP + i]; }
+      }
+    } else if (h.spec.sampler == MMB_SAMPLER_AMM) {
+      std::vector<double> mv, mvv, ls;
+      std::vector<uint8_t> pv;
+      if ((rc = d2h(e, mv, h.Mv, K * DP)) || (rc = d2h(e, mvv, h.Mvv, K * TP)) ||
+          (rc = d2h(e, ls, h.Ls, K * TP)) || (rc = d2h(e, pv, h.piv, K * DP)))
+        return rc;
+      for (int64_t k = 0; k < K; ++k) {
+        double* t = tune + k * TL + off;
+        t[0] = (fl[k] & 1) ? 1.0 : 0.0;
+        t[1] = m[k];
+        t[2] = (fl[k] & 4) ? 1.0 : 0.0;
+        t[3] = (fl[k] & 2) ? 1.0 : 0.0;
+        double* p = t + 4;
+        for (int i = 0; i < h.d; ++i) p[i] = mv[k * DP + i];
+        p += h.d;
+        for (int s = 0; s < h.T; ++s) p[s] = mvv[k * TP + s];
+        p += h.T;
+        for (int s = 0; s < h.T; ++s) p[s] = ls[k * TP + s];
+        p += h.T;
+        for (int i = 0; i < h.d; ++i) p[i] = pv[k * DP + i];
+      }
+    }
+    off += h.tune_len;
+  }
+  return 0;
+}
+
+int mmb_set_tune(mmb_engine* e, const double* tune) {
+  if (!e || !tune) return fail(e, MMB_E_ARG, "null argument");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  const int64_t TL = mmb_tune_len(e), K = e->K;
+  const size_t DP = e->DP, TP = e->TP;
+  int64_t off = 0;
+  for (auto& h : e->blocks) {
+    std::vector<int32_t> m(K, 0), fl(K, 0);
+    int rc;
+    if (h.spec.sampler == MMB_SAMPLER_AMWG) {
+      std::vector<double> sg(K * DP, 0.0), ac(K * DP, 0.0);
+      for (int64_t k = 0; k < K; ++k) {
+        const double* t = tune + k * TL + off;
+        fl[k] = t[0] != 0.0 ? 1 : 0;
+        m[k] = (int32_t)t[1];
+        for (int i = 0; i < h.d; ++i) { sg[k * DP + i] = t[2 + i]; ac[k * DP + i] = t[2 + h.d + i]; }
+      }
+      if ((rc = h2d(e, h.sigma, sg)) || (rc = h2d(e, h.accept, ac))) return rc;
+    } else if (h.spec.sampler == MMB_SAMPLER_AMM) {
+      std::vector<double> mv(K * DP, 0.0), mvv(K * TP, 0.0), ls(K * TP, 0.0);
+      std::vector<uint8_t> pv(K * DP, 0);
+      for (int64_t k = 0; k < K; ++k) {
+        const double* t = tune + k * TL + off;
+        fl[k] = (t[0] != 0.0 ? 1 : 0) | (t[2] != 0.0 ? 4 : 0) | (t[3] != 0.0 ? 2 : 0);
+        m[k] = (int32_t)t[1];
+        const double* p = t + 4;
+        for (int i = 0; i < h.d; ++i) mv[k * DP + i] = p[i];
+        p += h.d;
+        for (int s = 0; s < h.T; ++s) mvv[k * TP + s] = p[s];
+        p += h.T;
+        for (int s = 0; s < h.T; ++s) ls[k * TP + s] = p[s];
+        p += h.T;
+        for (int i = 0; i < h.d; ++i) pv[k * DP + i] = (uint8_t)p[i];
+      }
+      if ((rc = h2d(e, h.Mv, mv)) || (rc = h2d(e, h.Mvv, mvv)) || (rc = h2d(e, h.Ls, ls)) ||
+          (rc = h2d(e, h.piv, pv)))
+        return rc;
+    }
+    if ((rc = h2d(e, h.m, m)) || (rc = h2d(e, h.flags, fl))) return rc;
+    off += h.tune_len;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- Gelman-Rubin partials
+int64_t mmb_gr_len(const mmb_engine* e) {
+  if (!e) return MMB_E_ARG;
+  const int64_t p = e->pmon;
+  return 1 + p + p * p + p * p + 3 * p;
+}
+
+int mmb_gr_range(mmb_engine* e, double* minmax) {
+  if (!e || !minmax) return fail(e, MMB_E_ARG, "null argument");
+  if (e->n_kept < 1) return fail(e, MMB_E_STATE, "no device-kept draws (run with keep_device=1)");
+  HIPCHK(e, hipSetDevice(e->device));
+  double* d = nullptr;
+  HIPCHK(e, hipMalloc(&d, 2 * e->pmon * sizeof(double)));
+  hipError_t st = mmb_launch_gr_range(e->pmon, e->n_kept, (int)e->K, e->d_draws, d, e->stream);
+  if (st != hipSuccess) { (void)hipFree(d); return fail(e, MMB_E_HIP, "gr_range: %s", hipGetErrorString(st)); }
+  HIPCHK(e, hipMemcpyAsync(minmax, d, 2 * e->pmon * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipFree(d));
+  return 0;
+}
+
+int mmb_gr_partials(mmb_engine* e, const int32_t* link, const double* shift, double* out) {
+  if (!e || !link || !shift || !out) return fail(e, MMB_E_ARG, "null argument");
+  if (e->n_kept < 2) return fail(e, MMB_E_STATE, "need >= 2 device-kept draws per chain");
+  HIPCHK(e, hipSetDevice(e->device));
+  const int p = e->pmon;
+  const int64_t L = mmb_gr_len(e);
+  int32_t* dl = nullptr;
+  double *ds = nullptr, *dout = nullptr;
+  HIPCHK(e, hipMalloc(&dl, p * sizeof(int32_t)));
+  HIPCHK(e, hipMalloc(&ds, p * sizeof(double)));
+  HIPCHK(e, hipMalloc(&dout, L * sizeof(double)));
+  HIPCHK(e, hipMemcpyAsync(dl, link, p * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(ds, shift, p * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  hipError_t st = mmb_launch_gr_stats(p, e->n_kept, (int)e->K, e->d_draws, dl, ds, dout, e->stream);
+  if (st != hipSuccess) return fail(e, MMB_E_HIP, "gr_stats: %s", hipGetErrorString(st));
+  HIPCHK(e, hipMemcpyAsync(out, dout, L * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  (void)hipFree(dl);
+  (void)hipFree(ds);
+  (void)hipFree(dout);
+  return 0;
+}
+
+// ---------------------------------------------------------------- timing
+int mmb_sync(mmb_engine* e) {
+  if (!e) return fail(e, MMB_E_ARG, "null argument");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int mmb_kernel_time(const mmb_engine* e, double* total_ms, int64_t* launches, int64_t* units) {
+  if (!e) return MMB_E_ARG;
+  if (total_ms) *total_ms = e->kernel_ms;
+  if (launches) *launches = e->launches;
+  if (units) *units = e->units;
+  return 0;
+}
+
+// Algorithmic HBM bytes per chain-update (B = 2*S_state + S_draw/thin is
+// reported by bench.py; this returns 2*S_state with the minimal state: FP64 values,
+// packed symmetric matrices, int32 counters, one byte per pivot index).
+int mmb_state_bytes(const mmb_engine* e, double* bytes) {
+  if (!e || !bytes) return MMB_E_ARG;
+  double s = 8.0 * e->P;
+  for (auto& h : e->blocks) {
+    switch (h.spec.sampler) {
+      case MMB_SAMPLER_AMWG: s += 8.0 * h.d * 2 + 4.0 * h.d * 0 + 4.0; break;  // sigma, accept, m
+      case MMB_SAMPLER_AMM: s += 8.0 * (h.d + 2.0 * h.T) + 1.0 * h.d + 4.0; break;  // Mv, Mvv, L, piv, m
+      case MMB_SAMPLER_NUTS: s += 8.0 * 7 + 4.0; break;
+      default: break;
+    }
+  }
+  *bytes = 2.0 * s;
+  return 0;
+}
+

@@ -1,0 +1,320 @@
+// models.h — lowered model kernels: per-chain state, unlist/relist, block logpdf!,
+// conjugate Gibbs draws.  One specialisation per model kind.
+//
+// logf() restates logpdf!(m, x, block, transform) (src/model/simulation.jl:77-90):
+// params \ targets in block order with early exit on a non-finite sum, then the
+// block's targets in topological order; node densities per
+// src/distributions/distributionstruct.jl:136-168 and transformdistribution.jl:53-78.
+#pragma once
+#include "device.h"
+
+template <int MODEL>
+struct Mdl;
+
+// ------------------------------------------------------------------ rats
+// doc/examples/rats.jl:48-97.  Device value layout per chain (72 doubles):
+//   [0,32) alpha (30 + pad) | [32,64) beta | 64 s2_c | 65 mu_alpha | 66 s2_alpha |
+//   67 mu_beta | 68 s2_beta.   Group = 32 lanes, lane i <-> rat i.
+template <>
+struct Mdl<MMB_MODEL_RATS> {
+  static constexpr int G = 32, R = 1, DMAX = 30, DP = 32, TP = 480, VS = 72, PMON = 3;
+  static constexpr int LDS_DBL = TP + 4 * DP;  // packed matrix + 4 vectors (+ int scratch inside)
+  struct St { double a, b, s2c, mua, s2a, mub, s2b; };
+  struct Lc { double y[5]; };
+
+  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc& l) {
+    const double* v = A.vals + (size_t)c * VS;
+    s.a = v[lane];
+    s.b = v[32 + lane];
+    s.s2c = v[64]; s.mua = v[65]; s.s2a = v[66]; s.mub = v[67]; s.s2b = v[68];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) l.y[t] = lane < 30 ? A.data0[lane * 5 + t] : 0.0;
+  }
+  __device__ __forceinline__ static void store(const SweepArgs& A, int c, int lane, const St& s) {
+    double* v = A.vals + (size_t)c * VS;
+    v[lane] = s.a;
+    v[32 + lane] = s.b;
+    if (lane == 0) { v[64] = s.s2c; v[65] = s.mua; v[66] = s.s2a; v[67] = s.mub; v[68] = s.s2b; }
+  }
+  __device__ __forceinline__ static void monitored(const SweepArgs& A, const St& s, double* out) {
+    out[0] = s.s2c;
+    out[1] = s.mub;
+    out[2] = s.mua - A.xbar * s.mub;  // alpha0 = mu_alpha - xbar * mu_beta (rats.jl:65-67)
+  }
+  __device__ __forceinline__ static bool is_vec(int node) { return node == MMB_RATS_ALPHA || node == MMB_RATS_BETA; }
+  __device__ __forceinline__ static bool positive(int node) {
+    return node == MMB_RATS_S2_C || node == MMB_RATS_S2_ALPHA || node == MMB_RATS_S2_BETA;
+  }
+  // select chains (a switch here is turned into a dynamically indexed private array)
+  __device__ __forceinline__ static double scalar(const St& s, int node) {
+    double v = s.s2b;
+    v = node == MMB_RATS_S2_C ? s.s2c : v;
+    v = node == MMB_RATS_MU_ALPHA ? s.mua : v;
+    v = node == MMB_RATS_S2_ALPHA ? s.s2a : v;
+    v = node == MMB_RATS_MU_BETA ? s.mub : v;
+    return v;
+  }
+  __device__ __forceinline__ static void set_scalar(St& s, int node, double v) {
+    s.s2c = node == MMB_RATS_S2_C ? v : s.s2c;
+    s.mua = node == MMB_RATS_MU_ALPHA ? v : s.mua;
+    s.s2a = node == MMB_RATS_S2_ALPHA ? v : s.s2a;
+    s.mub = node == MMB_RATS_MU_BETA ? v : s.mub;
+    s.s2b = node == MMB_RATS_S2_BETA ? v : s.s2b;
+  }
+  __device__ __forceinline__ static int lane_node(const DBlock& B, int lane) {
+    int n = B.nodes[0];
+    n = lane == 1 ? B.nodes[1] : n;
+    n = lane == 2 ? B.nodes[2] : n;
+    n = lane == 3 ? B.nodes[3] : n;
+    return n;
+  }
+  // unlist(block, transform) into lane-owned element slots
+  __device__ __forceinline__ static void unlist(const DBlock& B, const St& s, int lane, double* x) {
+    if (is_vec(B.nodes[0])) {
+      x[0] = lane < 30 ? (B.nodes[0] == MMB_RATS_ALPHA ? s.a : s.b) : 0.0;
+    } else {
+      int n = lane_node(B, lane);
+      double v = scalar(s, n);
+      x[0] = lane < B.d ? ((B.transform && positive(n)) ? mmb_log(v) : v) : 0.0;
+    }
+  }
+  __device__ __forceinline__ static void relist(const DBlock& B, St& s, const Grp<G>& g, const double* x) {
+    if (is_vec(B.nodes[0])) {
+      if (B.nodes[0] == MMB_RATS_ALPHA) s.a = g.lane < 30 ? x[0] : s.a;
+      else s.b = g.lane < 30 ? x[0] : s.b;
+    } else {
+      for (int e = 0; e < B.d; ++e) {
+        double v = g.bcast(x[0], e);
+        int n = B.nodes[e];
+        set_scalar(s, n, (B.transform && positive(n)) ? mmb_exp(v) : v);
+      }
+    }
+  }
+  // lane partial of sum_t (y - (alpha + beta*Xm))^2 for this lane's rat
+  __device__ __forceinline__ static double ssr_lane(const SweepArgs& A, const Lc& l, double a, double b, int lane) {
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      double mu = a + b * A.xm[t];
+      double r = l.y[t] - mu;
+      acc = fma(r, r, acc);
+    }
+    return lane < 30 ? acc : 0.0;
+  }
+  __device__ __forceinline__ static double normsum_lane(double mu, double sig, double logsig, double x, int lane) {
+    return lane < 30 ? d_normlogpdf(mu, sig, logsig, x) : 0.0;
+  }
+  // logpdf!(block, x)
+  __device__ __forceinline__ static double logf(const SweepArgs& A, const DBlock& B, const St& s0, const Lc& l,
+                                const Grp<G>& g, const double* x) {
+    St s = s0;
+    relist(B, s, g, x);
+    const double NEG = -__builtin_inf();
+    if (is_vec(B.nodes[0])) {  // [alpha] or [beta]: prior (params\targets) then y
+      bool al = B.nodes[0] == MMB_RATS_ALPHA;
+      double mu = al ? s.mua : s.mub;
+      double sig = sqrt(al ? s.s2a : s.s2b);
+      double ls = mmb_log(sig);
+      double pr = normsum_lane(mu, sig, ls, al ? s.a : s.b, g.lane);
+      double ss = ssr_lane(A, l, s.a, s.b, g.lane);
+      g.sum2(pr, ss);
+      double lp = 0.0 + pr;
+      if (!isfinite(lp)) return lp;
+      return lp + d_iso(150, sqrt(s.s2c), ss);
+    }
+    // scalar block: params (none is a target of another) in block order
+    unsigned tm = 0;
+    double lp = 0.0;
+    bool stop = false;
+    for (int a = 0; a < B.nn; ++a) {
+      int n = B.nodes[a];
+      tm |= (n == MMB_RATS_S2_C) ? 4u : (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_S2_ALPHA) ? 1u : 2u;
+      if (stop) continue;
+      double t = positive(n) ? d_iglogpdf(A.ig_c, scalar(s, n), B.transform)
+                             : d_normlogpdf(0.0, 1000.0, mmb_log(1000.0), scalar(s, n));
+      lp += t;
+      if (!isfinite(lp)) stop = true;
+    }
+    if (stop) return lp;
+    // targets in topological order: alpha, beta, y
+    if (tm & 1u) {
+      double sig = sqrt(s.s2a);
+      double v = normsum_lane(s.mua, sig, mmb_log(sig), s.a, g.lane);
+      lp += g.sum(v);
+      if (!isfinite(lp)) return lp;
+    }
+    if (tm & 2u) {
+      double sig = sqrt(s.s2b);
+      double v = normsum_lane(s.mub, sig, mmb_log(sig), s.b, g.lane);
+      lp += g.sum(v);
+      if (!isfinite(lp)) return lp;
+    }
+    if (tm & 4u) {
+      double ss = g.sum(ssr_lane(A, l, s.a, s.b, g.lane));
+      lp += d_iso(150, sqrt(s.s2c), ss);
+    }
+    return lp;
+    (void)NEG;
+  }
+  // conjugate full conditionals (Gibbs_s2_c, Gibbs_mu_*, Gibbs_s2_*)
+  __device__ __forceinline__ static void gibbs(const SweepArgs& A, const DBlock& B, St& s, const Lc& l,
+                               const Grp<G>& g, const mmb_rng* rn, const mmb_rng* gn,
+                               const mmb_rng* gu) {
+    int n = B.nodes[0];
+    uint32_t kn = 0, ku = 0;
+    if (n == MMB_RATS_S2_C) {
+      double ss = g.sum(ssr_lane(A, l, s.a, s.b, g.lane));
+      double a = 150.0 / 2.0 + 0.001, b = ss / 2.0 + 0.001;
+      s.s2c = b / mmb_gamma_mt(a, gn, gu, &kn, &ku);
+    } else if (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_MU_BETA) {
+      bool al = n == MMB_RATS_MU_ALPHA;
+      double sum = g.sum(g.lane < 30 ? (al ? s.a : s.b) : 0.0);
+      double s2 = al ? s.s2a : s.s2b;
+      double var0 = 1000.0 * 1000.0;
+      double vv = 1.0 / (30.0 / s2 + 1.0 / var0);
+      double mean = vv * (sum / s2 + 0.0 / var0);
+      double v = mean + sqrt(vv) * mmb_normal(rn, 0u);
+      if (al) s.mua = v; else s.mub = v;
+    } else {
+      bool al = n == MMB_RATS_S2_ALPHA;
+      double mu = al ? s.mua : s.mub;
+      double r = (al ? s.a : s.b) - mu;
+      double ss = g.sum(g.lane < 30 ? r * r : 0.0);
+      double v = (ss / 2.0 + 0.001) / mmb_gamma_mt(30.0 / 2.0 + 0.001, gn, gu, &kn, &ku);
+      if (al) s.s2a = v; else s.s2b = v;
+    }
+  }
+};
+
+// ------------------------------------------------------------------ line
+// doc/tutorial/line.jl:5-25.  Device layout per chain: [b1, b2, s2, pad].  G = 1.
+template <>
+struct Mdl<MMB_MODEL_LINE> {
+  static constexpr int G = 1, R = 3, DMAX = 3, DP = 4, TP = 8, VS = 4, PMON = 3;
+  static constexpr int LDS_DBL = TP + 4 * DP;
+  struct St { double v[3]; };
+  struct Lc { int dummy; };
+
+  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int, St& s, Lc&) {
+    const double* v = A.vals + (size_t)c * VS;
+    s.v[0] = v[0]; s.v[1] = v[1]; s.v[2] = v[2];
+  }
+  __device__ __forceinline__ static void store(const SweepArgs& A, int c, int, const St& s) {
+    double* v = A.vals + (size_t)c * VS;
+    v[0] = s.v[0]; v[1] = s.v[1]; v[2] = s.v[2];
+  }
+  __device__ __forceinline__ static void monitored(const SweepArgs&, const St& s, double* out) {
+    out[0] = s.v[0]; out[1] = s.v[1]; out[2] = s.v[2];
+  }
+  __device__ __forceinline__ static double pick(const St& s, int vi) {
+    return vi == 0 ? s.v[0] : vi == 1 ? s.v[1] : s.v[2];
+  }
+  __device__ __forceinline__ static void unlist(const DBlock& B, const St& s, int, double* x) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      int vi = B.emap[r];
+      double v = pick(s, vi);
+      x[r] = r < B.d ? ((B.transform && vi == 2) ? mmb_log(v) : v) : 0.0;
+    }
+  }
+  __device__ __forceinline__ static void relist(const DBlock& B, St& s, const Grp<G>&, const double* x) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < B.d) {
+        int vi = B.emap[r];
+        double v = (B.transform && vi == 2) ? mmb_exp(x[r]) : x[r];
+        if (vi == 0) s.v[0] = v;
+        else if (vi == 1) s.v[1] = v;
+        else s.v[2] = v;
+      }
+    }
+  }
+  __device__ __forceinline__ static double ylp(const SweepArgs& A, const St& s) {
+    double ssq = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double mu = s.v[0] + A.lx[i] * s.v[1];
+      double r = A.ly[i] - mu;
+      ssq += r * r;
+    }
+    return d_iso(5, sqrt(s.v[2]), ssq);
+  }
+  __device__ __forceinline__ static double logf(const SweepArgs& A, const DBlock& B, const St& s0, const Lc&,
+                                const Grp<G>& g, const double* x) {
+    St s = s0;
+    relist(B, s, g, x);
+    double lp = 0.0;
+    for (int a = 0; a < B.nn; ++a) {
+      double t;
+      if (B.nodes[a] == MMB_LINE_BETA) {
+        if (!isfinite(s.v[0]) || !isfinite(s.v[1])) t = -__builtin_inf();
+        else t = d_iso(2, sqrt(1000.0), s.v[0] * s.v[0] + s.v[1] * s.v[1]);
+      } else {
+        t = d_iglogpdf(A.ig_c, s.v[2], B.transform);
+      }
+      lp += t;
+      if (!isfinite(lp)) return lp;
+    }
+    return lp + ylp(A, s);  // targets: mu (logical, 0), y
+  }
+  // analytic gradient (reference: Calculus forward differences, simulation.jl:47-51)
+  __device__ __forceinline__ static double logf_grad(const SweepArgs& A, const DBlock& B, const St& s0,
+                                     const double* x, double* gr) {
+    St s = s0;
+    Grp<G> g;
+    relist(B, s, g, x);
+    double lp = logf(A, B, s0, Lc{}, g, x);
+    double s2 = s.v[2];
+    double sr = 0.0, sxr = 0.0, ssq = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double mu = s.v[0] + A.lx[i] * s.v[1];
+      double r = A.ly[i] - mu;
+      sr += r;
+      sxr = fma(A.lx[i], r, sxr);
+      ssq = fma(r, r, ssq);
+    }
+    double sb = sqrt(1000.0);
+    double ivb = 1.0 / (sb * sb);
+    gr[0] = sr / s2 - s.v[0] * ivb;
+    gr[1] = sxr / s2 - s.v[1] * ivb;
+    gr[2] = B.d == 3 ? -(0.001 + 2.5) + (0.5 * ssq + 0.001) / s2 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if (!isfinite(gr[k])) gr[k] = 0.0;
+    return lp;
+  }
+  __device__ __forceinline__ static void gibbs(const SweepArgs& A, const DBlock& B, St& s, const Lc&,
+                               const Grp<G>&, const mmb_rng* rn, const mmb_rng* gn,
+                               const mmb_rng* gu) {
+    if (B.nodes[0] == MMB_LINE_BETA) {  // line.jl:168-177
+      double s2 = s.v[2];
+      double sb = sqrt(1000.0);
+      double ic = 1.0 / (sb * sb);
+      double sx = 0.0, sxx = 0.0, sy = 0.0, sxy = 0.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        sx += A.lx[i]; sxx += A.lx[i] * A.lx[i]; sy += A.ly[i]; sxy += A.lx[i] * A.ly[i];
+      }
+      double a = 5.0 / s2 + ic, b = sx / s2, dd = sxx / s2 + ic;
+      double det = a * dd - b * b;
+      double S11 = dd / det, S12 = -b / det, S22 = a / det;
+      double r1 = sy / s2, r2 = sxy / s2;
+      double m1 = S11 * r1 + S12 * r2, m2 = S12 * r1 + S22 * r2;
+      double l11 = sqrt(S11), l21 = S12 / l11, l22 = sqrt(S22 - l21 * l21);
+      double z0, z1;
+      mmb_normal_pair(rn, 0u, &z0, &z1);
+      s.v[0] = m1 + l11 * z0;
+      s.v[1] = m2 + (l21 * z0 + l22 * z1);
+    } else {  // line.jl:179-186
+      double ssq = 0.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        double r = A.ly[i] - (s.v[0] + A.lx[i] * s.v[1]);
+        ssq += r * r;
+      }
+      uint32_t kn = 0, ku = 0;
+      s.v[2] = (ssq / 2.0 + 0.001) / mmb_gamma_mt(5.0 / 2.0 + 0.001, gn, gu, &kn, &ku);
+    }
+  }
+};

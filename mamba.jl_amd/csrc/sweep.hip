@@ -1,0 +1,85 @@
+// sweep.hip — the fused block-sweep kernel: one launch advances every chain of the
+// shard through `n_iters` iterations of sample!(m) (simulation.jl:93-107), i.e.
+// mcmc_worker!'s loop body (mcmc.jl:74-80) including the keep rule and the
+// Chains write sim[i,:,1] = unlist(m, true) (mcmc.jl:76-77).
+//
+// Per chain, per iteration: values are held in registers; AMWG/AMM tune state
+// and the AMM moment/factor matrices are streamed from/to HBM (chain-major,
+// element fastest, coalesced per lane group); the AMM covariance and its
+// pivoted Cholesky factor are staged in LDS.
+#include "samplers.h"
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void sweep_kernel(const SweepArgs A) {
+  using M = Mdl<MODEL>;
+  using S = Smp<M>;
+  constexpr int G = M::G;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
+  if (c >= A.K) return;  // whole lane groups exit together
+  Grp<G> g;
+  double* lds = smem + (size_t)(threadIdx.x / G) * M::LDS_DBL;
+  typename M::St s;
+  typename M::Lc l;
+  M::load(A, c, g.lane, s, l);
+  const uint32_t chain = A.chain_offset + (uint32_t)c;
+  for (int step = 0; step < A.n_iters; ++step) {
+    const int64_t it = A.iter0 + 1 + step;
+    for (int b = 0; b < A.nb; ++b) {
+      const DBlock& B = A.blocks[b];  // global memory, uniform index
+      const mmb_rng rn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_NORMAL);
+      const mmb_rng ru = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_UNIFORM);
+      const bool adapt = B.adapt == MMB_ADAPT_ALL ? true
+                         : B.adapt == MMB_ADAPT_BURNIN ? (it <= A.model_burnin) : false;
+      switch (B.kind) {
+        case MMB_SAMPLER_AMWG:
+          S::amwg(A, B, c, rn, ru, adapt, s, l, g);
+          break;
+        case MMB_SAMPLER_AMM:
+          S::amm(A, B, c, rn, ru, adapt, s, l, g, lds);
+          break;
+        case MMB_SAMPLER_SLICE:
+          if (B.form == MMB_SLICE_UNIVARIATE) S::slice_uni(A, B, ru, s, l, g);
+          else S::slice_multi(A, B, ru, s, l, g);
+          break;
+        case MMB_SAMPLER_GIBBS: {
+          const mmb_rng gn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_N);
+          const mmb_rng gu = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_U);
+          M::gibbs(A, B, s, l, g, &rn, &gn, &gu);
+          break;
+        }
+        default:
+          break;
+      }
+    }
+    if (A.draws && it > A.burnin && (it - A.burnin) % A.thin == 0 && g.lane == 0) {
+      const int64_t row = (it - A.burnin) / A.thin - 1 - A.kept_origin;
+      double mon[M::PMON];
+      M::monitored(A, s, mon);
+#pragma unroll
+      for (int j = 0; j < M::PMON; ++j) A.draws[(size_t)(row * M::PMON + j) * A.K + c] = mon[j];
+    }
+  }
+  M::store(A, c, g.lane, s);
+}
+
+// host-side launcher (engine.cpp)
+hipError_t mmb_launch_sweep(int model, const SweepArgs& A, hipStream_t st) {
+  if (model == MMB_MODEL_RATS) {
+    using M = Mdl<MMB_MODEL_RATS>;
+    const int threads = 256, per_block = threads / M::G;
+    const int blocks = (A.K + per_block - 1) / per_block;
+    const size_t lds = (size_t)per_block * M::LDS_DBL * sizeof(double);
+    hipLaunchKernelGGL(sweep_kernel<MMB_MODEL_RATS>, dim3(blocks), dim3(threads), lds, st, A);
+    return hipGetLastError();
+  }
+  if (model == MMB_MODEL_LINE) {
+    using M = Mdl<MMB_MODEL_LINE>;
+    const int threads = 64, per_block = threads / M::G;
+    const int blocks = (A.K + per_block - 1) / per_block;
+    const size_t lds = (size_t)per_block * M::LDS_DBL * sizeof(double);
+    hipLaunchKernelGGL(sweep_kernel<MMB_MODEL_LINE>, dim3(blocks), dim3(threads), lds, st, A);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}

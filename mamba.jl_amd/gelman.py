@@ -1,0 +1,110 @@
+"""Gelman, Rubin and Brooks diagnostic (src/output/gelmandiag.jl:3-60), sharded.
+
+The device reduces each chain's kept draws to the sufficient statistics of
+gelmandiag (Engine.gr_partials); those L-vectors are summed over GPUs with one
+RCCL all-reduce (torch.distributed, backend "nccl"); this module turns the global
+sums into the PSRF / upper limit / MPSRF exactly as gelmandiag.jl does.
+
+L-vector layout for p monitored params (phi = chain mean - shift):
+  [m, sum phi (p), sum phi phi' (p*p), sum S2 (p*p), sum s2^2 (p), sum s2*phi (p), sum s2*phi^2 (p)]
+"""
+import numpy as np
+from scipy import stats
+
+
+def link_kinds(minmax):
+    """link(c) (src/output/chains.jl:237-246): log for positive, logit if also < 1."""
+    kinds = []
+    for lo, hi in minmax:
+        kinds.append(0 if not lo > 0.0 else (2 if hi < 1.0 else 1))
+    return np.array(kinds, dtype=np.int32)
+
+
+def psrf_from_sums(sums, n, p, alpha=0.05, mpsrf=False):
+    sums = np.asarray(sums, dtype=np.float64)
+    o = 0
+    m = sums[o]; o += 1
+    A1 = sums[o:o + p]; o += p
+    A2 = sums[o:o + p * p].reshape(p, p); o += p * p
+    A3 = sums[o:o + p * p].reshape(p, p); o += p * p
+    A4 = sums[o:o + p]; o += p
+    A5 = sums[o:o + p]; o += p
+    A6 = sums[o:o + p]
+    if m < 2:
+        raise ValueError("less than 2 chains supplied to gelman diagnostic")
+    W = A3 / m
+    mphi = A1 / m
+    covpsi = (A2 - m * np.outer(mphi, mphi)) / (m - 1)
+    B = n * covpsi
+    w, b = np.diag(W), np.diag(B)
+    s2sum = np.diag(A3)
+    phi2sum = np.diag(A2)
+    var_w = ((A4 - s2sum**2 / m) / (m - 1)) / m
+    var_b = (2.0 / (m - 1)) * b**2
+    cov_s2_phi2 = (A6 - s2sum * phi2sum / m) / (m - 1)
+    cov_s2_phi = (A5 - s2sum * A1 / m) / (m - 1)
+    var_wb = (n / m) * (cov_s2_phi2 - 2.0 * mphi * cov_s2_phi)
+    V = ((n - 1) / n) * w + ((m + 1) / (m * n)) * b
+    var_V = ((n - 1)**2 * var_w + ((m + 1) / m)**2 * var_b + (2.0 * (n - 1) * (m + 1) / m) * var_wb) / n**2
+    df = 2.0 * V**2 / var_V
+    B_df = m - 1
+    W_df = 2.0 * w**2 / var_w
+    R_fixed = (n - 1) / n
+    R_random_scale = (m + 1) / (m * n)
+    q = 1.0 - alpha / 2.0
+    psrf = np.empty((p, 2))
+    for i in range(p):
+        corr = (df[i] + 3.0) / (df[i] + 1.0)
+        R_random = R_random_scale * b[i] / w[i]
+        psrf[i, 0] = np.sqrt(corr * (R_fixed + R_random))
+        if not np.isnan(R_random):
+            R_random *= stats.f.ppf(q, B_df, W_df[i])
+        psrf[i, 1] = np.sqrt(corr * (R_fixed + R_random))
+    mp = None
+    if mpsrf:
+        try:
+            np.linalg.cholesky(W)
+            mp = R_fixed + R_random_scale * float(np.max(np.real(np.linalg.eigvals(np.linalg.solve(W, B)))))
+        except np.linalg.LinAlgError:
+            mp = float("nan")
+    return psrf, mp
+
+
+def gelmandiag_sharded(engine, allreduce_sum=None, allreduce_minmax=None, transform=False,
+                       alpha=0.05, mpsrf=False):
+    """PSRF over all chains of all ranks.  `allreduce_sum(x)` / `allreduce_minmax(lo, hi)`
+    perform the cross-GPU reductions (identity on a single engine)."""
+    p = engine.pmon
+    mm = engine.gr_range()
+    lo, hi = mm[:, 0].copy(), mm[:, 1].copy()
+    if allreduce_minmax is not None:
+        lo, hi = allreduce_minmax(lo, hi)
+    kinds = link_kinds(zip(lo, hi)) if transform else np.zeros(p, dtype=np.int32)
+    mid = 0.5 * (lo + hi)
+    shift = np.where(kinds == 1, np.log(np.maximum(mid, 1e-300)),
+                     np.where(kinds == 2, np.log(mid / (1 - mid)), mid))
+    local = engine.gr_partials(kinds, shift)
+    tot = allreduce_sum(local) if allreduce_sum is not None else local
+    n = engine.lib.mmb_num_kept(engine.h)
+    return psrf_from_sums(tot, n, p, alpha=alpha, mpsrf=mpsrf)
+
+
+def gelmandiag(chains, alpha=0.05, mpsrf=False, transform=False):
+    """Host gelmandiag on an n x p x m array (reference formula, gelmandiag.jl:3-60)."""
+    psi = np.asarray(chains.value if hasattr(chains, "value") else chains, dtype=np.float64)
+    n, p, m = psi.shape
+    if m < 2:
+        raise ValueError("less than 2 chains supplied to gelman diagnostic")
+    if transform:
+        psi = psi.copy()
+        for j in range(p):
+            x = psi[:, j, :]
+            if x.min() > 0:
+                psi[:, j, :] = np.log(x / (1 - x)) if x.max() < 1 else np.log(x)
+    means = psi.mean(0)                               # p x m
+    S2 = np.einsum("ijk,ilk->jlk", psi - means, psi - means) / (n - 1)
+    phi = means.T                                     # m x p
+    s2 = np.stack([np.diag(S2[:, :, k]) for k in range(m)])
+    sums = np.concatenate([[m], phi.sum(0), (phi.T @ phi).ravel(), S2.sum(2).ravel(),
+                           (s2**2).sum(0), (s2 * phi).sum(0), (s2 * phi**2).sum(0)])
+    return psrf_from_sums(sums, n, p, alpha=alpha, mpsrf=mpsrf)

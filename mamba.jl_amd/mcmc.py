@@ -1,0 +1,188 @@
+"""mcmc() driver, Engine wrapper and Chains container.
+
+Mirrors src/model/mcmc.jl: `mcmc(m, inputs, inits, iters; burnin, thin, chains)`
+(mcmc.jl:19-33) and the restart form `mcmc(mc, iters)` (mcmc.jl:3-16).  The chain
+fan-out (`pmap2(mcmc_worker!, ...)`, mcmc.jl:52) is one HIP engine per GPU holding a
+contiguous shard of global chain ids; draws come back in Mamba's Chains layout
+(n x p x chains, src/output/chains.jl:5-11).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .samplers import ArgumentError
+
+
+class Engine:
+    """One libmambahip engine (one GPU, one shard of chains)."""
+
+    def __init__(self, model, device=0):
+        self.lib = abi.lib()
+        self.model = model
+        self.spec = model.spec()
+        h = C.c_void_p()
+        rc = self.lib.mmb_create(C.byref(self.spec), int(device), C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"mmb_create failed ({abi.ERRORS.get(rc, rc)}): "
+                               f"{self.lib.mmb_last_error(None).decode()}")
+        self.h = h
+        for name, arr in zip(model.input_names, model.data_arrays()):
+            self._chk(self.lib.mmb_set_data(self.h, name.encode(), abi.dptr(arr), arr.size))
+        self.P = self.lib.mmb_num_values(self.h)
+        self.pmon = self.lib.mmb_num_monitored(self.h)
+        self.K = 0
+
+    def _chk(self, rc):
+        return abi.check(rc, self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mmb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def init_chains(self, init, chain_offset=0, seed=1):
+        init = np.ascontiguousarray(init, dtype=np.float64)
+        self.K = init.shape[0]
+        self._chk(self.lib.mmb_init_chains(self.h, abi.dptr(init), self.K, int(chain_offset),
+                                           C.c_uint64(int(seed))))
+
+    def run(self, iters, burnin=0, thin=1, model_burnin=None, draws=True, keep_device=False,
+            time_kernels=False):
+        a = abi.RunArgs()
+        a.iters, a.burnin, a.thin = int(iters), int(burnin), int(thin)
+        a.model_burnin = int(burnin if model_burnin is None else model_burnin)
+        a.keep_device = int(keep_device)
+        a.time_kernels = int(time_kernels)
+        it0 = self.iter
+        kept = lambda t: (t - burnin) // thin if t > burnin else 0  # noqa: E731
+        nk = kept(it0 + iters) - kept(it0)
+        out = None
+        if draws and nk > 0:
+            out = np.empty((nk, self.pmon, self.K), order="F")
+            a.draws = abi.dptr(out)
+        self._chk(self.lib.mmb_run(self.h, C.byref(a)))
+        return out
+
+    @property
+    def iter(self):
+        return self.lib.mmb_iter(self.h)
+
+    def values(self):
+        v = np.empty((self.K, self.P))
+        self._chk(self.lib.mmb_get_values(self.h, abi.dptr(v)))
+        return v
+
+    def set_values(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        self._chk(self.lib.mmb_set_values(self.h, abi.dptr(v)))
+
+    def tune(self):
+        n = self.lib.mmb_tune_len(self.h)
+        t = np.empty((self.K, max(n, 1)))
+        if n > 0:
+            self._chk(self.lib.mmb_get_tune(self.h, abi.dptr(t)))
+        return t[:, :n]
+
+    def set_tune(self, t):
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        if t.size:
+            self._chk(self.lib.mmb_set_tune(self.h, abi.dptr(t)))
+
+    def draws(self):
+        nk = self.lib.mmb_num_kept(self.h)
+        out = np.empty((nk, self.pmon, self.K), order="F")
+        if nk:
+            self._chk(self.lib.mmb_get_draws(self.h, abi.dptr(out)))
+        return out
+
+    def sync(self):
+        self._chk(self.lib.mmb_sync(self.h))
+
+    def kernel_time(self):
+        ms = C.c_double()
+        n = C.c_int64()
+        u = C.c_int64()
+        self.lib.mmb_kernel_time(self.h, C.byref(ms), C.byref(n), C.byref(u))
+        return ms.value, n.value, u.value
+
+    def state_bytes(self):
+        b = C.c_double()
+        self.lib.mmb_state_bytes(self.h, C.byref(b))
+        return b.value
+
+    # Gelman-Rubin partial sums of the device-kept draws (for the cross-GPU all-reduce)
+    def gr_range(self):
+        mm = np.empty(2 * self.pmon)
+        self._chk(self.lib.mmb_gr_range(self.h, abi.dptr(mm)))
+        return mm.reshape(self.pmon, 2)
+
+    def gr_partials(self, link, shift):
+        link = np.ascontiguousarray(link, dtype=np.int32)
+        shift = np.ascontiguousarray(shift, dtype=np.float64)
+        out = np.empty(self.lib.mmb_gr_len(self.h))
+        self._chk(self.lib.mmb_gr_partials(self.h, link.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           abi.dptr(shift), abi.dptr(out)))
+        return out
+
+
+class Chains:
+    """Chains / ModelChains (src/output/chains.jl:5-11, modelchains.jl): value is
+    n x p x chains, names the monitored nodes, range = start:thin:stop."""
+
+    def __init__(self, value, names, start, thin, chains, model=None, engine=None):
+        self.value = value
+        self.names = list(names)
+        self.start, self.thin = int(start), int(thin)
+        self.chains = np.asarray(chains)
+        self.model = model
+        self.engine = engine
+
+    @property
+    def range(self):
+        n = self.value.shape[0]
+        return range(self.start, self.start + n * self.thin, self.thin)
+
+    def __getitem__(self, name):
+        return self.value[:, self.names.index(name), :]
+
+    def describe(self):
+        v = self.value
+        return {nm: {"mean": float(v[:, j, :].mean()), "sd": float(v[:, j, :].std(ddof=1))}
+                for j, nm in enumerate(self.names)}
+
+
+def mcmc(model, inputs, inits, iters, burnin=0, thin=1, chains=1, verbose=False, device=0,
+         chain_offset=0, seed=1, keep_device=False):
+    """mcmc(m, inputs, inits, iters; burnin, thin, chains) (mcmc.jl:19-33)."""
+    if not iters > burnin:
+        raise ArgumentError("burnin is greater than or equal to iters")
+    model.setinputs(inputs)
+    init = model.init_matrix(inits, chains)
+    model.burnin = burnin
+    eng = Engine(model, device)
+    eng.init_chains(init, chain_offset=chain_offset, seed=seed)
+    draws = eng.run(iters, burnin=burnin, thin=thin, model_burnin=burnin, keep_device=keep_device)
+    if draws is None:
+        draws = np.empty((0, eng.pmon, eng.K))
+    model.iter = eng.iter
+    return Chains(draws, model.monitor_names, burnin + thin, thin,
+                  np.arange(chain_offset + 1, chain_offset + chains + 1), model, eng)
+
+
+def mcmc_restart(mc, iters, verbose=False):
+    """mcmc(mc::ModelChains, iters) (mcmc.jl:3-16): continue from model.states."""
+    eng, model = mc.engine, mc.model
+    last = mc.range[-1] if mc.value.shape[0] else mc.start - mc.thin
+    if last != (model.iter // mc.thin) * mc.thin:
+        raise ArgumentError("chain is missing its last iteration")
+    draws = eng.run(iters, burnin=last, thin=mc.thin, model_burnin=model.burnin)
+    model.iter = eng.iter
+    value = np.concatenate([mc.value, draws], axis=0) if draws is not None else mc.value
+    return Chains(value, mc.names, mc.start, mc.thin, mc.chains, model, eng)

@@ -1,0 +1,101 @@
+"""Sampler constructors mirroring Mamba.jl's model-based sampler API.
+
+Each constructor returns a `Sampler` (src/Mamba.jl:119-124: params, eval, tune,
+targets) whose `eval` is a lowered HIP block update instead of a Julia closure.
+Argument meaning, defaults and validation errors follow the reference:
+
+  AMWG(params, sigma; adapt=:all, batchsize=50, target=0.44)   src/samplers/amwg.jl:47-61
+  AMM(params, Sigma; adapt=:all, beta=0.05, scale=2.38)        src/samplers/amm.jl:160-174
+  NUTS(params; dtype=:forward, target=0.6)                     src/samplers/nuts.jl:47-56
+  Slice(params, width, Univariate|Multivariate; transform=false) src/samplers/slice.jl:252-263
+  Gibbs(params)  -- a user `Sampler(params, f)` whose f is the node's conjugate full
+                    conditional (doc/tutorial/line.jl:168-186); lowered per model.
+"""
+import numpy as np
+
+from . import abi
+
+Univariate = "Univariate"
+Multivariate = "Multivariate"
+
+
+class ArgumentError(ValueError):
+    """Julia ArgumentError raised by the reference's validators."""
+
+
+def _params(params):
+    if isinstance(params, str):
+        return [params]
+    return list(params)
+
+
+def _adapt(adapt):
+    adapt = str(adapt).lstrip(":")
+    if adapt not in ("all", "burnin", "none"):
+        raise ArgumentError("adapt must be one of :all, :burnin, or :none")
+    return {"all": abi.MMB_ADAPT_ALL, "burnin": abi.MMB_ADAPT_BURNIN, "none": abi.MMB_ADAPT_NONE}[adapt]
+
+
+class Sampler:
+    def __init__(self, params, kind, adapt=abi.MMB_ADAPT_ALL, tuning=None, **kw):
+        self.params = _params(params)
+        self.kind = kind
+        self.adapt = adapt
+        self.tuning = None if tuning is None else np.atleast_1d(np.asarray(tuning, dtype=np.float64))
+        self.form = kw.pop("form", abi.MMB_SLICE_MULTIVARIATE)
+        self.transform = int(kw.pop("transform", False))
+        self.batchsize = int(kw.pop("batchsize", 50))
+        self.target = float(kw.pop("target", 0.44))
+        self.beta = float(kw.pop("beta", 0.05))
+        self.scale = float(kw.pop("scale", 2.38))
+        if kw:
+            raise ArgumentError(f"unsupported sampler arguments {sorted(kw)}")
+        self.targets = []
+
+    def validate(self, dim):
+        """validate(v) (amwg.jl:37-42, amm.jl:150-155, slice.jl:237-247)"""
+        t = self.tuning
+        if self.kind == abi.MMB_SAMPLER_AMWG and not (t.size == 1 or t.size == dim):
+            raise ArgumentError(f"length(sigma) differs from variate length {dim}")
+        if self.kind == abi.MMB_SAMPLER_AMM and t.size != dim * dim:
+            raise ArgumentError(f"Sigma dimension differs from variate length {dim}")
+        if self.kind == abi.MMB_SAMPLER_SLICE and not (t.size == 1 or t.size == dim):
+            raise ArgumentError(f"length(width) differs from variate length {dim}")
+
+    def __repr__(self):
+        names = {1: "AMWG", 2: "AMM", 3: "NUTS", 4: "Slice", 5: "Gibbs"}
+        return f"{names[self.kind]}({self.params})"
+
+
+def AMWG(params, sigma, adapt="all", batchsize=50, target=0.44):
+    return Sampler(params, abi.MMB_SAMPLER_AMWG, _adapt(adapt), sigma, batchsize=batchsize,
+                   target=target)
+
+
+def AMM(params, Sigma, adapt="all", beta=0.05, scale=2.38):
+    S = np.asarray(Sigma, dtype=np.float64)
+    if S.ndim != 2 or S.shape[0] != S.shape[1]:
+        raise ArgumentError("Sigma must be a square matrix")
+    # column-major, as Julia stores it
+    return Sampler(params, abi.MMB_SAMPLER_AMM, _adapt(adapt), S.ravel(order="F"), beta=beta,
+                   scale=scale)
+
+
+def NUTS(params, dtype="forward", target=0.6):
+    # dtype selects Calculus' finite-difference scheme in the reference; the lowered
+    # models supply analytic gradients, so it is accepted and ignored.
+    if str(dtype).lstrip(":") not in ("forward", "central", "complex"):
+        raise ArgumentError(f"unsupported dtype {dtype}")
+    return Sampler(params, abi.MMB_SAMPLER_NUTS, abi.MMB_ADAPT_BURNIN, None, target=target)
+
+
+def Slice(params, width, form=Multivariate, transform=False):
+    f = {Univariate: abi.MMB_SLICE_UNIVARIATE, Multivariate: abi.MMB_SLICE_MULTIVARIATE}.get(form)
+    if f is None:
+        raise ArgumentError("form must be Univariate or Multivariate")
+    return Sampler(params, abi.MMB_SAMPLER_SLICE, abi.MMB_ADAPT_NONE, width, form=f,
+                   transform=transform)
+
+
+def Gibbs(params):
+    return Sampler(params, abi.MMB_SAMPLER_GIBBS, abi.MMB_ADAPT_NONE, None)

@@ -1,0 +1,82 @@
+"""C ABI boundary checks that run without a GPU: the library loads, exports every
+symbol include/mamba_hip.h declares, the ctypes structs match the header layout, and
+argument validation (ArgumentError semantics of the reference) happens host-side."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "mamba_hip.h")
+
+
+def declared_symbols():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*]+\s+)+\**(mmb_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol(mamba):
+    lib = mamba.abi.lib()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", mamba.abi.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (mmb_\w+)", out))
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    assert lib.mmb_abi_version() == 1
+
+
+def test_struct_layout_matches_header(mamba):
+    src = """
+#include <stddef.h>
+#include <stdio.h>
+#include "mamba_hip.h"
+int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(mmb_block_spec), sizeof(mmb_model_spec),
+ sizeof(mmb_run_args), offsetof(mmb_block_spec, tuning), offsetof(mmb_model_spec, prior_sd),
+ offsetof(mmb_run_args, keep_device)); return 0;}
+"""
+    d = "/tmp/mmb_layout"
+    os.makedirs(d, exist_ok=True)
+    open(f"{d}/t.c", "w").write(src)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", f"{d}/t", f"{d}/t.c"])
+    got = list(map(int, subprocess.check_output([f"{d}/t"]).split()))
+    a = mamba.abi
+    want = [C.sizeof(a.BlockSpec), C.sizeof(a.ModelSpec), C.sizeof(a.RunArgs), a.BlockSpec.tuning.offset,
+            a.ModelSpec.prior_sd.offset, a.RunArgs.keep_device.offset]
+    assert got == want
+
+
+def test_create_validates_before_touching_the_device(mamba):
+    lib = mamba.abi.lib()
+    m = mamba.line()
+    m.setsamplers([mamba.AMWG(["beta", "s2"], 1.0)])
+    sp = m.spec()
+    sp.blocks[0].dim = 7                      # wrong block length
+    h = C.c_void_p()
+    assert lib.mmb_create(C.byref(sp), 0, C.byref(h)) == -1
+    assert b"unlisted length" in lib.mmb_last_error(None)
+    sp = m.spec()
+    sp.blocks[0].sampler = 3                  # NUTS not lowered for line in this version
+    rc = lib.mmb_create(C.byref(sp), 0, C.byref(h))
+    assert rc in (-2, 0, -3)
+    r = mamba.rats()
+    r.setsamplers([mamba.Slice(["alpha", "mu_alpha"], 1.0)])   # mixed vector/scalar block
+    assert lib.mmb_create(C.byref(r.spec()), 0, C.byref(h)) == -2
+
+
+def test_python_argument_errors(mamba):
+    with pytest.raises(mamba.ArgumentError, match="adapt must be one of"):
+        mamba.AMWG("alpha", 1.0, adapt="sometimes")
+    m = mamba.rats()
+    with pytest.raises(mamba.ArgumentError, match="length\\(sigma\\) differs"):
+        m.setsamplers([mamba.AMWG("alpha", [1.0, 2.0])])
+    with pytest.raises(mamba.ArgumentError, match="Sigma dimension"):
+        m.setsamplers([mamba.AMM("alpha", np.eye(3))])
+    with pytest.raises(mamba.ArgumentError, match="burnin is greater"):
+        mamba.mcmc(m.setsamplers([mamba.Gibbs("s2_c")]), mamba.model.RATS_DATA, mamba.model.RATS_INITS, 10,
+                   burnin=10)
+    with pytest.raises(mamba.ArgumentError, match="fewer initial values"):
+        m.setinputs(mamba.model.RATS_DATA).init_matrix(mamba.model.RATS_INITS, 3)

