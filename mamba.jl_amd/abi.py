@@ -44,7 +44,7 @@ class RunArgs(C.Structure):
 
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmambahip.so")
+LIB_PATH = os.environ.get("MMB_LIB") or os.path.join(PKG_DIR, "lib", "libmambahip.so")
 _lib = None
 
 

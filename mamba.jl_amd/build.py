@@ -19,28 +19,30 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
 
 
-def _compile(src, objdir):
+def _compile(src, objdir, defines=()):
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
-    cmd = [HIPCC, *FLAGS, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj
 
 
-def build(verbose=False):
-    objdir = os.path.join(PKG, "lib", "obj")
+def build(verbose=False, out=OUT, defines=()):
+    """defines: extra -D flags (experiments, e.g. MMB_SWEEP_WAVES=3) -> separate obj dir."""
+    tag = "_".join(d.replace("=", "") for d in defines)
+    objdir = os.path.join(PKG, "lib", "obj" + ("_" + tag if tag else ""))
     os.makedirs(objdir, exist_ok=True)
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     with ThreadPoolExecutor(max_workers=4) as ex:
-        objs = list(ex.map(lambda s: _compile(s, objdir), srcs))
-    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT]
+        objs = list(ex.map(lambda s: _compile(s, objdir, defines), srcs))
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     if verbose:
-        print("built", OUT)
-    return OUT
+        print("built", out)
+    return out
 
 
 if __name__ == "__main__":

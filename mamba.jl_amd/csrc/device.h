@@ -66,16 +66,74 @@ __device__ __forceinline__ void grp_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- cross-lane primitives for 32-lane groups: DPP / permlane (no LDS round trip) ----
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  uint64_t u = mmb_d2u(x);
+  int lo = dpp_i<CTRL>((int)(uint32_t)u), hi = dpp_i<CTRL>((int)(uint32_t)(u >> 32));
+  return mmb_u2d((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32));
+}
+// value of lane ^ 16 (rows 0<->1 and 2<->3 of the wave)
+__device__ __forceinline__ int swap16_i(int x) {
+  auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+  return (int)((threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ double swap16_d(double x) {
+  uint64_t u = mmb_d2u(x);
+  int lo = swap16_i((int)(uint32_t)u), hi = swap16_i((int)(uint32_t)(u >> 32));
+  return mmb_u2d((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32));
+}
+// stage s of the 32-lane all-reduce: partner lanes xor1, xor2 (quad_perm), 7-i (row_half_mirror),
+// 15-i (row_mirror), i^16 (permlane16_swap).  After stage s every lane of the 2^(s+1) subgroup
+// holds the same (commutative) combination.
+#define MMB_DPP_XOR1 0xB1
+#define MMB_DPP_XOR2 0x4E
+#define MMB_DPP_HMIRROR 0x141
+#define MMB_DPP_MIRROR 0x140
+
 template <int G>
 struct Grp {
   int lane;
   __device__ __forceinline__ Grp() : lane((int)(threadIdx.x & (G - 1))) {}
+  template <int S>
+  __device__ __forceinline__ static double other_d(double x) {
+    if (S == 0) return dpp_d<MMB_DPP_XOR1>(x);
+    if (S == 1) return dpp_d<MMB_DPP_XOR2>(x);
+    if (S == 2) return dpp_d<MMB_DPP_HMIRROR>(x);
+    if (S == 3) return dpp_d<MMB_DPP_MIRROR>(x);
+    return swap16_d(x);
+  }
+  template <int S>
+  __device__ __forceinline__ static int other_i(int x) {
+    if (S == 0) return dpp_i<MMB_DPP_XOR1>(x);
+    if (S == 1) return dpp_i<MMB_DPP_XOR2>(x);
+    if (S == 2) return dpp_i<MMB_DPP_HMIRROR>(x);
+    if (S == 3) return dpp_i<MMB_DPP_MIRROR>(x);
+    return swap16_i(x);
+  }
   __device__ __forceinline__ double sum(double x) const {
+    if (G == 32) {
+      x += other_d<0>(x); x += other_d<1>(x); x += other_d<2>(x); x += other_d<3>(x);
+      x += other_d<4>(x);
+      return x;
+    }
 #pragma unroll
     for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
     return x;
   }
   __device__ __forceinline__ void sum2(double& x, double& y) const {
+    if (G == 32) {
+      x += other_d<0>(x); y += other_d<0>(y);
+      x += other_d<1>(x); y += other_d<1>(y);
+      x += other_d<2>(x); y += other_d<2>(y);
+      x += other_d<3>(x); y += other_d<3>(y);
+      x += other_d<4>(x); y += other_d<4>(y);
+      return;
+    }
 #pragma unroll
     for (int m = G / 2; m >= 1; m >>= 1) {
       double a = __shfl_xor(x, m, 64);
@@ -94,16 +152,29 @@ struct Grp {
     int base = (int)(threadIdx.x & 63) & ~(G - 1);
     return __shfl(x, base + src, 64);
   }
-  // Lexicographic (key desc, pos asc) argmax; carries value and index.
-  __device__ __forceinline__ void argmax(double& key, int& pos, double& val, int& idx) const {
+  template <int S>
+  __device__ __forceinline__ static void amax_stage(double& key, int& pi) {
+    double ok = other_d<S>(key);
+    int op = other_i<S>(pi);
+    bool take = (ok > key) || (ok == key && op < pi);
+    key = take ? ok : key;
+    pi = take ? op : pi;
+  }
+  // Lexicographic argmax: larger key wins, ties -> smaller position.  pi = pos << 16 | idx
+  // (pos, idx < 2^15), so comparing pi compares positions.
+  __device__ __forceinline__ void argmax(double& key, int& pi) const {
+    if (G == 32) {
+      amax_stage<0>(key, pi); amax_stage<1>(key, pi); amax_stage<2>(key, pi);
+      amax_stage<3>(key, pi); amax_stage<4>(key, pi);
+      return;
+    }
 #pragma unroll
     for (int m = G / 2; m >= 1; m >>= 1) {
       double ok = __shfl_xor(key, m, 64);
-      int op = __shfl_xor(pos, m, 64);
-      double ov = __shfl_xor(val, m, 64);
-      int oi = __shfl_xor(idx, m, 64);
-      bool take = (ok > key) || (ok == key && op < pos);
-      if (take) { key = ok; pos = op; val = ov; idx = oi; }
+      int op = __shfl_xor(pi, m, 64);
+      bool take = (ok > key) || (ok == key && op < pi);
+      key = take ? ok : key;
+      pi = take ? op : pi;
     }
   }
 };

@@ -17,7 +17,7 @@
 #include "device.h"
 #include "models.h"
 
-hipError_t mmb_launch_sweep(int model, const SweepArgs& A, hipStream_t st);
+hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
                                hipStream_t st);
 hipError_t mmb_launch_gr_stats(int pmon, int64_t n, int K, const double* draws, const int32_t* link,
@@ -45,6 +45,7 @@ struct mmb_engine {
   int model = 0;
   int P = 0, pmon = 0, VS = 0, DP = 0, TP = 0;
   std::vector<BlockHost> blocks;
+  unsigned kinds = 0;  // bitmask of sampler kinds in the scheme
   // data
   std::vector<double> x, y, X;
   bool have_data = false;
@@ -61,6 +62,7 @@ struct mmb_engine {
   int64_t n_kept = 0;
   // timing
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> evpool;  // 2 per launch when time_kernels
   double kernel_ms = 0.0;
   int64_t launches = 0, units = 0;
   std::string err;
@@ -237,6 +239,7 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
         return fail(nullptr, MMB_E_ARG, "unknown sampler kind %d", s.sampler);
     }
     h.tune_len = tune_len_of(s.sampler, d);
+    e->kinds |= 1u << s.sampler;
     e->blocks.push_back(h);
   }
   hipError_t st = hipSetDevice(device);
@@ -280,6 +283,7 @@ void mmb_destroy(mmb_engine* e) {
   if (e->d_data) (void)hipFree(e->d_data);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
+  for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -523,22 +527,32 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
   e->kernel_ms = 0.0;
   e->launches = 0;
   e->units = 0;
-  for (int64_t done = 0; done < a->iters; done += W) {
+  const int64_t nl = (a->iters + W - 1) / W;
+  if (a->time_kernels) {
+    while ((int64_t)e->evpool.size() < 2 * nl) {
+      hipEvent_t ev;
+      HIPCHK(e, hipEventCreate(&ev));
+      e->evpool.push_back(ev);
+    }
+  }
+  for (int64_t done = 0, li = 0; done < a->iters; done += W, ++li) {
     int w = (int)std::min<int64_t>(W, a->iters - done);
     A.iter0 = it0 + done;
     A.n_iters = w;
-    if (a->time_kernels) HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-    hipError_t st = mmb_launch_sweep(e->model, A, e->stream);
+    if (a->time_kernels) HIPCHK(e, hipEventRecord(e->evpool[2 * li], e->stream));
+    hipError_t st = mmb_launch_sweep(e->model, e->kinds, A, e->stream);
     if (st != hipSuccess) return fail(e, MMB_E_HIP, "sweep launch: %s", hipGetErrorString(st));
-    if (a->time_kernels) {
-      HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-      HIPCHK(e, hipEventSynchronize(e->ev1));
-      float ms = 0.f;
-      HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-      e->kernel_ms += ms;
-    }
+    if (a->time_kernels) HIPCHK(e, hipEventRecord(e->evpool[2 * li + 1], e->stream));
     e->launches += 1;
     e->units += (int64_t)w * e->K;
+  }
+  if (a->time_kernels) {  // per-launch device time, summed after the window (no per-launch sync)
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    for (int64_t li = 0; li < nl; ++li) {
+      float ms = 0.f;
+      HIPCHK(e, hipEventElapsedTime(&ms, e->evpool[2 * li], e->evpool[2 * li + 1]));
+      e->kernel_ms += ms;
+    }
   }
   e->iter = it0 + a->iters;
   e->n_kept = want ? nk : 0;

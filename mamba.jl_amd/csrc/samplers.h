@@ -80,13 +80,17 @@ struct Smp {
   }
 
   // ---------------------------------------------------------------- pivoted Cholesky
-  // cholfact(Hermitian(S), Val{true}) restated as LAPACK dpstf2('U', tol = 0) op order
-  // (see oracle.c orc_pchol).  S: packed symmetric in LDS (`mat`, slot(i,k));
-  // factored in place: L[i][step k] ends in slot(i, piv[k]), L[i][pos_i] in slot(i,i).
-  // pk[] receives the pivot order.  Returns the rank (group-uniform).
-  __device__ __forceinline__ static int pchol(int d, double* mat, int* pk, const Grp<G>& g) {
+  // cholfact(Hermitian(S), Val{true}) restated in LAPACK dpstf2('U', tol = 0) op order
+  // (oracle.c orc_pchol): pivot = first maximum of the remaining diagonal in position
+  // order, stop when it is <= 0 or NaN, row J as a dot product then scaled by ONE/AJJ.
+  // The dot product runs on two accumulators (even / odd k) summed at the end (the
+  // oracle does the same).  S: packed symmetric in LDS (`mat`, slot(i,k)); the pivot's
+  // factor row is broadcast through `prow` (contiguous LDS) each step.  On full rank the
+  // factor is written back in place: L[i][step k] -> slot(i, piv[k]), L[i][pos_i] ->
+  // slot(i,i).  pk[] receives the pivot order.  Returns the rank (group-uniform).
+  __device__ __forceinline__ static int pchol(int d, double* mat, double* prow, int* pks,
+                                              const Grp<G>& g) {
     double diag0[R], work[R], Lrow[R][DMAX];
-    int posv[R];
     bool done[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -94,53 +98,130 @@ struct Smp {
       done[r] = !(e < d);
       diag0[r] = e < d ? mat[mmb_tri(e) + e] : 0.0;
       work[r] = 0.0;
-      posv[r] = e;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) Lrow[r][k] = 0.0;
     }
     int rank = d;
     bool live = true;
 #pragma unroll
     for (int j = 0; j < DMAX; ++j) {
       if (live && j < d) {
-        double key = -__builtin_inf(), val = __builtin_nan("");
-        int pos = 0x7fffffff, idx = -1;
+        // ---- pivot: first maximum of the remaining diagonal in position order ----
+        double dl[R], cand[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if (!done[r]) {
-            double dd = diag0[r] - work[r];
-            double kk = isnan(dd) ? (posv[r] == j ? __builtin_inf() : -__builtin_inf()) : dd;
-            if (kk > key || (kk == key && posv[r] < pos)) {
-              key = kk; pos = posv[r]; val = dd; idx = r * G + g.lane;
+          dl[r] = diag0[r] - work[r];
+          cand[r] = done[r] ? -__builtin_inf() : dl[r];
+        }
+        int p;
+        double val;
+        if (G == 32) {
+          // fast path: max-reduce, then the (usually unique) lane holding it
+          double mx = cand[0];
+          bool anynan = isnan(mx);
+          mx = anynan ? -__builtin_inf() : mx;
+          mx = fmax(mx, Grp<G>::template other_d<0>(mx));
+          mx = fmax(mx, Grp<G>::template other_d<1>(mx));
+          mx = fmax(mx, Grp<G>::template other_d<2>(mx));
+          mx = fmax(mx, Grp<G>::template other_d<3>(mx));
+          mx = fmax(mx, Grp<G>::template other_d<4>(mx));
+          const unsigned long long bw = __ballot(!done[0] && cand[0] == mx);
+          const unsigned long long bn = __ballot(!done[0] && anynan);
+          const unsigned sh = threadIdx.x & 32;
+          const unsigned win = (unsigned)(bw >> sh), nan_ = (unsigned)(bn >> sh);
+          if (__builtin_popcount(win) == 1 && nan_ == 0) {
+            p = __builtin_ctz(win);
+            val = mx;
+          } else {
+            // rare: exact tie or NaN -> replay dpstf2's position swaps (pks history)
+            int* perm = (int*)prow;  // group-private LDS scratch
+            if (g.lane == 0) {
+              for (int t = 0; t < d; ++t) perm[t] = t;
+              for (int k = 0; k < j; ++k) {
+                int q = pks[k], qpos = k;
+                for (int t = k; t < d; ++t) if (perm[t] == q) qpos = t;
+                int tmp = perm[k]; perm[k] = q; perm[qpos] = tmp;
+              }
+            }
+            grp_sync();
+            int mypos = 0x7fffffff;
+            for (int t = j; t < d; ++t) if (perm[t] == g.lane) mypos = t;
+            grp_sync();
+            double key = done[0] ? -__builtin_inf()
+                                 : (isnan(dl[0]) ? (mypos == j ? __builtin_inf() : -__builtin_inf()) : dl[0]);
+            int pi = (done[0] ? 0x7fff : mypos) << 16 | g.lane;
+            g.argmax(key, pi);
+            p = pi & 0xffff;
+            val = g.bcast(dl[0], p);
+          }
+        } else {
+          // sequential lanes (G == 1): replay positions per chain
+          int perm[DMAX];
+#pragma unroll
+          for (int t = 0; t < DMAX; ++t) perm[t] = t;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) {
+            if (k < j) {
+              int q = pks[k];
+              int qpos = k;
+#pragma unroll
+              for (int t = 0; t < DMAX; ++t) qpos = (t >= k && perm[t] == q) ? t : qpos;
+              int tmp = perm[k];
+#pragma unroll
+              for (int t = 0; t < DMAX; ++t) perm[t] = (t == qpos) ? tmp : perm[t];
+              perm[k] = q;
             }
           }
+          // fold in position order: first strict maximum (oracle.c orc_pchol)
+          int best = -1;
+          double bv = 0.0;
+#pragma unroll
+          for (int t = 0; t < DMAX; ++t) {
+            if (t >= j && t < d) {
+              int e = perm[t];
+              double de = dl[0];
+#pragma unroll
+              for (int r = 1; r < R; ++r) de = (e == r) ? dl[r] : de;
+              if (best < 0) { best = e; bv = de; }
+              else if (de > bv) { best = e; bv = de; }
+            }
+          }
+          p = best;
+          val = bv;
         }
-        g.argmax(key, pos, val, idx);
         if (!(val > 0.0)) {
           rank = j;
           live = false;
         } else {
-          const int p = idx, ppos = pos;
-#pragma unroll
-          for (int r = 0; r < R; ++r) {  // swap positions j and ppos
-            int e = r * G + g.lane;
-            if (!done[r] && posv[r] == j) posv[r] = ppos;
-            if (e == p) { posv[r] = j; done[r] = true; }
-          }
-          pk[j] = p;
+          if (g.lane == 0) pks[j] = p;
           const double ajj = sqrt(val);
           const double rinv = 1.0 / ajj;
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            int e = r * G + g.lane;
-            if (e == p) {
+            if (r * G + g.lane == p) {
+              done[r] = true;
               Lrow[r][j] = ajj;
-              mat[mmb_tri(p) + p] = ajj;
-            } else if (!done[r]) {
-              double t = 0.0;
 #pragma unroll
-              for (int k = 0; k < j; ++k) t = fma(Lrow[r][k], mat[mmb_slot(p, pk[k])], t);
-              double lij = (mat[mmb_slot(e, p)] - t) * rinv;
+              for (int k = 0; k + 1 < j; k += 2)
+                *(double2*)(prow + k) = make_double2(Lrow[r][k], Lrow[r][k + 1]);
+              if (j & 1) prow[j - 1] = Lrow[r][j - 1];
+            }
+          }
+          grp_sync();
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            int e = r * G + g.lane;
+            if (!done[r]) {
+              double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+              for (int k = 0; k + 1 < j; k += 2) {
+                const double2 pp = *(const double2*)(prow + k);
+                t0 = fma(Lrow[r][k], pp.x, t0);
+                t1 = fma(Lrow[r][k + 1], pp.y, t1);
+              }
+              if (j & 1) t0 = fma(Lrow[r][j - 1], prow[j - 1], t0);
+              double lij = (mat[mmb_slot(e, p)] - (t0 + t1)) * rinv;
               Lrow[r][j] = lij;
-              mat[mmb_slot(e, p)] = lij;
               work[r] = work[r] + lij * lij;
             }
           }
@@ -148,13 +229,33 @@ struct Smp {
         }
       }
     }
+    if (rank == d) {  // write the factor back in slot form
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        int e = r * G + g.lane;
+        if (e < d) {
+          bool before = true;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) {
+            if (k < d) {
+              const int q = pks[k];
+              if (q == e) {
+                mat[mmb_tri(e) + e] = Lrow[r][k];
+                before = false;
+              } else if (before) {
+                mat[mmb_slot(e, q)] = Lrow[r][k];
+              }
+            }
+          }
+        }
+      }
+    }
     return rank;
   }
 
   __device__ __forceinline__ static void slot_ik(int s, int& i, int& k) {
-    int ii = (int)((sqrt(8.0 * (double)s + 1.0) - 1.0) * 0.5);
+    int ii = 0;
     while (mmb_tri(ii + 1) <= s) ++ii;
-    while (mmb_tri(ii) > s) --ii;
     i = ii;
     k = s - mmb_tri(ii);
   }
@@ -293,24 +394,27 @@ struct Smp {
         }
         grp_sync();
       }
+      int si, sk;  // (i, k) of slot g.lane, then stepped by G slots per iteration
+      slot_ik(g.lane, si, sk);
       for (int t = g.lane; t < T; t += G) {
-        int i, k;
-        slot_ik(t, i, k);
+        const int i = si, k = sk;
+        sk += G;
+        while (sk > si) { sk -= si + 1; ++si; }
         double old = fresh ? z2s[i] * z2s[k] : Mvv[t];
         double nv = p * old + (q * vvs[k]) * vvs[i];
         Mvv[t] = nv;
         mat[t] = cc * (nv - mvs[k] * mvs[i]);
       }
       grp_sync();
-      int pkv[DMAX];
-      int rank = pchol(d, mat, pkv, g);
+      int* pks = (int*)z2s;  // pivot order (group-uniform values), LDS
+      grp_sync();
+      int rank = pchol(d, mat, (double*)ia, pks, g);
+      grp_sync();
       if (rank == d) {
         double* Ls = B.t_Ls + (size_t)c * TP;
         for (int t = g.lane; t < T; t += G) Ls[t] = mat[t];
         uint8_t* pv = B.t_piv + (size_t)c * DP;
-#pragma unroll
-        for (int k = 0; k < DMAX; ++k)
-          if (k < d && g.lane == (k % G)) pv[k] = (uint8_t)pkv[k];
+        for (int k = g.lane; k < d; k += G) pv[k] = (uint8_t)pks[k];
         fl |= 4;
       }
     }

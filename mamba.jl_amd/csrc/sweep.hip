@@ -9,8 +9,14 @@
 // pivoted Cholesky factor are staged in LDS.
 #include "samplers.h"
 
-template <int MODEL>
-__global__ __launch_bounds__(256) void sweep_kernel(const SweepArgs A) {
+#ifndef MMB_SWEEP_WAVES
+#define MMB_SWEEP_WAVES 3  // min waves per SIMD the register allocator must allow
+#endif
+
+// KINDS: bitmask (1 << mmb_sampler_kind) of the sampler kinds present in the scheme; the
+// other block paths are compiled out (register/SGPR allocation is per kernel).
+template <int MODEL, unsigned KINDS>
+__global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const SweepArgs A) {
   using M = Mdl<MODEL>;
   using S = Smp<M>;
   constexpr int G = M::G;
@@ -33,21 +39,23 @@ __global__ __launch_bounds__(256) void sweep_kernel(const SweepArgs A) {
                          : B.adapt == MMB_ADAPT_BURNIN ? (it <= A.model_burnin) : false;
       switch (B.kind) {
         case MMB_SAMPLER_AMWG:
-          S::amwg(A, B, c, rn, ru, adapt, s, l, g);
+          if constexpr ((KINDS >> MMB_SAMPLER_AMWG) & 1u) S::amwg(A, B, c, rn, ru, adapt, s, l, g);
           break;
         case MMB_SAMPLER_AMM:
-          S::amm(A, B, c, rn, ru, adapt, s, l, g, lds);
+          if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) S::amm(A, B, c, rn, ru, adapt, s, l, g, lds);
           break;
         case MMB_SAMPLER_SLICE:
-          if (B.form == MMB_SLICE_UNIVARIATE) S::slice_uni(A, B, ru, s, l, g);
-          else S::slice_multi(A, B, ru, s, l, g);
+          if constexpr ((KINDS >> MMB_SAMPLER_SLICE) & 1u) {
+            if (B.form == MMB_SLICE_UNIVARIATE) S::slice_uni(A, B, ru, s, l, g);
+            else S::slice_multi(A, B, ru, s, l, g);
+          }
           break;
-        case MMB_SAMPLER_GIBBS: {
+        case MMB_SAMPLER_GIBBS: if constexpr ((KINDS >> MMB_SAMPLER_GIBBS) & 1u) {
           const mmb_rng gn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_N);
           const mmb_rng gu = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_U);
           M::gibbs(A, B, s, l, g, &rn, &gn, &gu);
-          break;
         }
+          break;
         default:
           break;
       }
@@ -63,23 +71,28 @@ __global__ __launch_bounds__(256) void sweep_kernel(const SweepArgs A) {
   M::store(A, c, g.lane, s);
 }
 
-// host-side launcher (engine.cpp)
-hipError_t mmb_launch_sweep(int model, const SweepArgs& A, hipStream_t st) {
+constexpr unsigned K_ALL = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_AMM) |
+                         (1u << MMB_SAMPLER_SLICE) | (1u << MMB_SAMPLER_GIBBS);
+constexpr unsigned K_GIBBS_AMM = (1u << MMB_SAMPLER_AMM) | (1u << MMB_SAMPLER_GIBBS);
+constexpr unsigned K_SLICE_AMWG = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_SLICE);
+
+template <int MODEL, unsigned KINDS>
+static hipError_t launch(const SweepArgs& A, hipStream_t st, int threads) {
+  using M = Mdl<MODEL>;
+  const int per_block = threads / M::G;
+  const int blocks = (A.K + per_block - 1) / per_block;
+  const size_t lds = (size_t)per_block * M::LDS_DBL * sizeof(double);
+  hipLaunchKernelGGL((sweep_kernel<MODEL, KINDS>), dim3(blocks), dim3(threads), lds, st, A);
+  return hipGetLastError();
+}
+
+// host-side launcher (engine.cpp); kinds = bitmask of the scheme's sampler kinds
+hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st) {
   if (model == MMB_MODEL_RATS) {
-    using M = Mdl<MMB_MODEL_RATS>;
-    const int threads = 256, per_block = threads / M::G;
-    const int blocks = (A.K + per_block - 1) / per_block;
-    const size_t lds = (size_t)per_block * M::LDS_DBL * sizeof(double);
-    hipLaunchKernelGGL(sweep_kernel<MMB_MODEL_RATS>, dim3(blocks), dim3(threads), lds, st, A);
-    return hipGetLastError();
+    if ((kinds & ~K_GIBBS_AMM) == 0) return launch<MMB_MODEL_RATS, K_GIBBS_AMM>(A, st, 256);
+    if ((kinds & ~K_SLICE_AMWG) == 0) return launch<MMB_MODEL_RATS, K_SLICE_AMWG>(A, st, 256);
+    return launch<MMB_MODEL_RATS, K_ALL>(A, st, 256);
   }
-  if (model == MMB_MODEL_LINE) {
-    using M = Mdl<MMB_MODEL_LINE>;
-    const int threads = 64, per_block = threads / M::G;
-    const int blocks = (A.K + per_block - 1) / per_block;
-    const size_t lds = (size_t)per_block * M::LDS_DBL * sizeof(double);
-    hipLaunchKernelGGL(sweep_kernel<MMB_MODEL_LINE>, dim3(blocks), dim3(threads), lds, st, A);
-    return hipGetLastError();
-  }
+  if (model == MMB_MODEL_LINE) return launch<MMB_MODEL_LINE, K_ALL>(A, st, 64);
   return hipErrorInvalidValue;
 }
