@@ -18,17 +18,16 @@ struct Mdl;
 template <>
 struct Mdl<MMB_MODEL_RATS> {
   static constexpr int G = 32, R = 1, DMAX = 30, DP = 32, TP = 480, VS = 72, PMON = 3;
-  static constexpr int LDS_DBL = TP + 4 * DP;  // packed matrix + 4 vectors (+ int scratch inside)
+  static constexpr int LDS_DBL = TP + 4 * DP + 2 * DP + 8;  // matrix, 4 vectors, state stash
   struct St { double a, b, s2c, mua, s2a, mub, s2b; };
-  struct Lc { double y[5]; };
+  struct Lc { const double* y; };  // this lane's 5 observations (global, L1-resident)
 
   __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc& l) {
     const double* v = A.vals + (size_t)c * VS;
     s.a = v[lane];
     s.b = v[32 + lane];
     s.s2c = v[64]; s.mua = v[65]; s.s2a = v[66]; s.mub = v[67]; s.s2b = v[68];
-#pragma unroll
-    for (int t = 0; t < 5; ++t) l.y[t] = lane < 30 ? A.data0[lane * 5 + t] : 0.0;
+    l.y = A.data0 + (lane < 30 ? lane : 0) * 5;
   }
   __device__ __forceinline__ static void store(const SweepArgs& A, int c, int lane, const St& s) {
     double* v = A.vals + (size_t)c * VS;
@@ -44,6 +43,22 @@ struct Mdl<MMB_MODEL_RATS> {
   __device__ __forceinline__ static bool is_vec(int node) { return node == MMB_RATS_ALPHA || node == MMB_RATS_BETA; }
   __device__ __forceinline__ static bool positive(int node) {
     return node == MMB_RATS_S2_C || node == MMB_RATS_S2_ALPHA || node == MMB_RATS_S2_BETA;
+  }
+  // park the chain state in LDS across a register-heavy phase (pivoted Cholesky)
+  static constexpr int STASH_DBL = 2 * DP + 8;
+  __device__ __forceinline__ static void stash(double* q, const St& s, int lane) {
+    q[lane] = s.a;
+    q[DP + lane] = s.b;
+    if (lane == 0) {
+      q[2 * DP + 0] = s.s2c; q[2 * DP + 1] = s.mua; q[2 * DP + 2] = s.s2a;
+      q[2 * DP + 3] = s.mub; q[2 * DP + 4] = s.s2b;
+    }
+  }
+  __device__ __forceinline__ static void unstash(const double* q, St& s, int lane) {
+    s.a = q[lane];
+    s.b = q[DP + lane];
+    s.s2c = q[2 * DP + 0]; s.mua = q[2 * DP + 1]; s.s2a = q[2 * DP + 2];
+    s.mub = q[2 * DP + 3]; s.s2b = q[2 * DP + 4];
   }
   // select chains (a switch here is turned into a dynamically indexed private array)
   __device__ __forceinline__ static double scalar(const St& s, int node) {
@@ -104,24 +119,50 @@ struct Mdl<MMB_MODEL_RATS> {
   __device__ __forceinline__ static double normsum_lane(double mu, double sig, double logsig, double x, int lane) {
     return lane < 30 ? d_normlogpdf(mu, sig, logsig, x) : 0.0;
   }
+  // Invariants of a vector block's logpdf! that do not depend on the block vector:
+  // prior sd / log sd of the block node and y's ScalMat constants.  Computed once per
+  // block update with the same operations logf would do, so results are bit-identical.
+  struct VecCtx { double mu, sig, logsig, yk; double invv; bool al; };
+  __device__ __forceinline__ static VecCtx vec_ctx(const DBlock& B, const St& s) {
+    VecCtx c;
+    c.al = B.nodes[0] == MMB_RATS_ALPHA;
+    c.mu = c.al ? s.mua : s.mub;
+    c.sig = sqrt(c.al ? s.s2a : s.s2b);
+    c.logsig = mmb_log(c.sig);
+    const double sc = sqrt(s.s2c);
+    const double value = sc * sc;
+    c.invv = 1.0 / value;
+    c.yk = 150 * MMB_LOG2PI + 150 * mmb_log(value);
+    return c;
+  }
+  // logpdf!([alpha] or [beta], x): prior (params \ targets) then y (d_iso expanded)
+  __device__ __forceinline__ static double logf_vec(const SweepArgs& A, const VecCtx& c,
+                                                    const St& s, const Lc& l, const Grp<G>& g,
+                                                    double x) {
+    const double a = c.al ? x : s.a, b = c.al ? s.b : x;
+    double pr = normsum_lane(c.mu, c.sig, c.logsig, x, g.lane);
+    double ss = ssr_lane(A, l, a, b, g.lane);
+    g.sum2(pr, ss);
+    double lp = 0.0 + pr;
+    if (!isfinite(lp)) return lp;
+    return lp + (-0.5 * (c.yk + ss * c.invv));
+  }
+  // block-update-invariant context (vector blocks); scalar blocks fall back to logf
+  using Prep = VecCtx;
+  __device__ __forceinline__ static Prep prep(const DBlock& B, const St& s) { return vec_ctx(B, s); }
+  __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep& c,
+                                                  const St& s, const Lc& l, const Grp<G>& g,
+                                                  const double* x) {
+    if (is_vec(B.nodes[0])) return logf_vec(A, c, s, l, g, x[0]);
+    return logf(A, B, s, l, g, x);
+  }
   // logpdf!(block, x)
   __device__ __forceinline__ static double logf(const SweepArgs& A, const DBlock& B, const St& s0, const Lc& l,
                                 const Grp<G>& g, const double* x) {
     St s = s0;
     relist(B, s, g, x);
     const double NEG = -__builtin_inf();
-    if (is_vec(B.nodes[0])) {  // [alpha] or [beta]: prior (params\targets) then y
-      bool al = B.nodes[0] == MMB_RATS_ALPHA;
-      double mu = al ? s.mua : s.mub;
-      double sig = sqrt(al ? s.s2a : s.s2b);
-      double ls = mmb_log(sig);
-      double pr = normsum_lane(mu, sig, ls, al ? s.a : s.b, g.lane);
-      double ss = ssr_lane(A, l, s.a, s.b, g.lane);
-      g.sum2(pr, ss);
-      double lp = 0.0 + pr;
-      if (!isfinite(lp)) return lp;
-      return lp + d_iso(150, sqrt(s.s2c), ss);
-    }
+    if (is_vec(B.nodes[0])) return logf_vec(A, vec_ctx(B, s0), s0, l, g, x[0]);
     // scalar block: params (none is a target of another) in block order
     unsigned tm = 0;
     double lp = 0.0;
@@ -191,9 +232,16 @@ struct Mdl<MMB_MODEL_RATS> {
 template <>
 struct Mdl<MMB_MODEL_LINE> {
   static constexpr int G = 1, R = 3, DMAX = 3, DP = 4, TP = 8, VS = 4, PMON = 3;
-  static constexpr int LDS_DBL = TP + 4 * DP;
+  static constexpr int LDS_DBL = TP + 4 * DP + 8;
   struct St { double v[3]; };
   struct Lc { int dummy; };
+  static constexpr int STASH_DBL = 8;
+  __device__ __forceinline__ static void stash(double* q, const St& s, int) {
+    q[0] = s.v[0]; q[1] = s.v[1]; q[2] = s.v[2];
+  }
+  __device__ __forceinline__ static void unstash(const double* q, St& s, int) {
+    s.v[0] = q[0]; s.v[1] = q[1]; s.v[2] = q[2];
+  }
 
   __device__ __forceinline__ static void load(const SweepArgs& A, int c, int, St& s, Lc&) {
     const double* v = A.vals + (size_t)c * VS;
@@ -228,6 +276,13 @@ struct Mdl<MMB_MODEL_LINE> {
         else s.v[2] = v;
       }
     }
+  }
+  struct Prep {};
+  __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
+  __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep&,
+                                                  const St& s, const Lc& l, const Grp<G>& g,
+                                                  const double* x) {
+    return logf(A, B, s, l, g, x);
   }
   __device__ __forceinline__ static double ylp(const SweepArgs& A, const St& s) {
     double ssq = 0.0;

@@ -34,7 +34,8 @@ struct Smp {
     fl = adapt ? (fl | 1) : (fl & ~1);
     const double ad = adapt ? 1.0 : 0.0;
     if (adapt) m += 1;
-    double logf0 = M::logf(A, B, s, l, g, x);
+    const typename M::Prep pc = M::prep(B, s);
+    double logf0 = M::logf_p(A, B, pc, s, l, g, x);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       int e = r * G + g.lane;
@@ -48,7 +49,7 @@ struct Smp {
         bool own = g.lane == ln;
         double xo = x[r];
         if (own) x[r] += z[r];
-        double lpp = M::logf(A, B, s, l, g, x);
+        double lpp = M::logf_p(A, B, pc, s, l, g, x);
         if (mmb_uniform(&ru, (uint32_t)e) < mmb_exp(lpp - logf0)) {
           logf0 = lpp;
           if (own) acc[r] += ad;
@@ -354,8 +355,9 @@ struct Smp {
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = x[r] + v[r];
-    double lx = M::logf(A, B, s, l, g, x);
-    double lv = M::logf(A, B, s, l, g, v);
+    const typename M::Prep pc = M::prep(B, s);
+    double lx = M::logf_p(A, B, pc, s, l, g, x);
+    double lv = M::logf_p(A, B, pc, s, l, g, v);
     if (mmb_uniform(&ru, 0u) < mmb_exp(lx - lv)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) v[r] = x[r];
@@ -406,6 +408,17 @@ struct Smp {
         mat[t] = cc * (nv - mvs[k] * mvs[i]);
       }
       grp_sync();
+      // everything but the factorization is finished first; the chain state is parked
+      // in LDS so the Cholesky's register footprint does not stack on top of it
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        int e = r * G + g.lane;
+        if (e < d) B.t_Mv[(size_t)c * DP + e] = mv[r];
+      }
+      if (g.lane == 0) { B.t_m[c] = m; B.t_flags[c] = fl; }
+      M::relist(B, s, g, v);
+      double* stq = lds + TP + 4 * DP;
+      M::stash(stq, s, g.lane);
       int* pks = (int*)z2s;  // pivot order (group-uniform values), LDS
       grp_sync();
       int rank = pchol(d, mat, (double*)ia, pks, g);
@@ -415,8 +428,11 @@ struct Smp {
         for (int t = g.lane; t < T; t += G) Ls[t] = mat[t];
         uint8_t* pv = B.t_piv + (size_t)c * DP;
         for (int k = g.lane; k < d; k += G) pv[k] = (uint8_t)pks[k];
-        fl |= 4;
+        if (g.lane == 0) B.t_flags[c] = fl | 4;
       }
+      M::unstash(stq, s, g.lane);
+      grp_sync();
+      return;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
