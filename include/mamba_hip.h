@@ -60,9 +60,9 @@ enum { MMB_LOGISTIC_BETA = 0 };
 /* ---- sampler kinds (src/samplers/{amwg,amm,nuts,slice}.jl) ---- */
 typedef enum {
   MMB_SAMPLER_AMWG = 1,  /* src/samplers/amwg.jl:47-61 */
-  MMB_SAMPLER_AMM = 2,   /* src/samplers/amm.jl:160-174 */
+  MMB_SAMPLER_AMM = 2,   /* src/samplers/amm.jl:45-59    */
   MMB_SAMPLER_NUTS = 3,  /* src/samplers/nuts.jl:47-56 */
-  MMB_SAMPLER_SLICE = 4, /* src/samplers/slice.jl:252-263 */
+  MMB_SAMPLER_SLICE = 4, /* src/samplers/slice.jl:47-58 */
   MMB_SAMPLER_GIBBS = 5  /* user Sampler(params, f): conjugate full conditional of the block's node,
                             e.g. doc/tutorial/line.jl:168-186 */
 } mmb_sampler_kind;

@@ -81,11 +81,12 @@ def gelmandiag_sharded(engine, allreduce_sum=None, allreduce_minmax=None, transf
         lo, hi = allreduce_minmax(lo, hi)
     kinds = link_kinds(zip(lo, hi)) if transform else np.zeros(p, dtype=np.int32)
     mid = 0.5 * (lo + hi)
-    shift = np.where(kinds == 1, np.log(np.maximum(mid, 1e-300)),
-                     np.where(kinds == 2, np.log(mid / (1 - mid)), mid))
+    shift = mid.copy()
+    shift[kinds == 1] = np.log(mid[kinds == 1])
+    shift[kinds == 2] = np.log(mid[kinds == 2] / (1.0 - mid[kinds == 2]))
     local = engine.gr_partials(kinds, shift)
     tot = allreduce_sum(local) if allreduce_sum is not None else local
-    n = engine.lib.mmb_num_kept(engine.h)
+    n = engine.num_kept()
     return psrf_from_sums(tot, n, p, alpha=alpha, mpsrf=mpsrf)
 
 

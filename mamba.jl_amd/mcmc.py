@@ -95,8 +95,11 @@ class Engine:
         if t.size:
             self._chk(self.lib.mmb_set_tune(self.h, abi.dptr(t)))
 
+    def num_kept(self):
+        return self.lib.mmb_num_kept(self.h)
+
     def draws(self):
-        nk = self.lib.mmb_num_kept(self.h)
+        nk = self.num_kept()
         out = np.empty((nk, self.pmon, self.K), order="F")
         if nk:
             self._chk(self.lib.mmb_get_draws(self.h, abi.dptr(out)))

@@ -5,9 +5,9 @@ targets) whose `eval` is a lowered HIP block update instead of a Julia closure.
 Argument meaning, defaults and validation errors follow the reference:
 
   AMWG(params, sigma; adapt=:all, batchsize=50, target=0.44)   src/samplers/amwg.jl:47-61
-  AMM(params, Sigma; adapt=:all, beta=0.05, scale=2.38)        src/samplers/amm.jl:160-174
+  AMM(params, Sigma; adapt=:all, beta=0.05, scale=2.38)        src/samplers/amm.jl:45-59
   NUTS(params; dtype=:forward, target=0.6)                     src/samplers/nuts.jl:47-56
-  Slice(params, width, Univariate|Multivariate; transform=false) src/samplers/slice.jl:252-263
+  Slice(params, width, Univariate|Multivariate; transform=false) src/samplers/slice.jl:47-58
   Gibbs(params)  -- a user `Sampler(params, f)` whose f is the node's conjugate full
                     conditional (doc/tutorial/line.jl:168-186); lowered per model.
 """
