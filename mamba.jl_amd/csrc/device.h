@@ -34,6 +34,7 @@ struct DBlock {
   double* t_Ls;          // AMM   [K][TP] factor, in-place slot storage
   uint8_t* t_piv;        // AMM   [K][DP] pivot order
   double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
+  double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
 };
 
 struct SweepArgs {

@@ -16,6 +16,7 @@
 
 #include "device.h"
 #include "models.h"
+#include "nuts.h"
 
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
@@ -33,7 +34,7 @@ struct BlockHost {
   bool sigl_diag = false;
   // device
   double *sigma = nullptr, *accept = nullptr, *Mv = nullptr, *Mvv = nullptr, *Ls = nullptr;
-  double *nuts = nullptr, *width = nullptr, *sigl_d = nullptr;
+  double *nuts = nullptr, *nfr = nullptr, *width = nullptr, *sigl_d = nullptr;
   int32_t *m = nullptr, *flags = nullptr;
   uint8_t* piv = nullptr;
 };
@@ -232,8 +233,11 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
         }
         break;
       case MMB_SAMPLER_NUTS:
-        delete e;
-        return fail(nullptr, MMB_E_UNSUPPORTED, "NUTS for this model is not lowered in this version");
+        if (e->model == MMB_MODEL_RATS) {
+          delete e;
+          return fail(nullptr, MMB_E_UNSUPPORTED, "NUTS for the rats model is not lowered in this version");
+        }
+        break;
       default:
         delete e;
         return fail(nullptr, MMB_E_ARG, "unknown sampler kind %d", s.sampler);
@@ -259,10 +263,10 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
 
 static void free_dev(mmb_engine* e) {
   for (auto& h : e->blocks) {
-    void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.width, h.sigl_d, h.m, h.flags, h.piv};
+    void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.nfr, h.width, h.sigl_d, h.m, h.flags, h.piv};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
-    h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.width = h.sigl_d = nullptr;
+    h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.nfr = h.width = h.sigl_d = nullptr;
     h.m = h.flags = nullptr;
     h.piv = nullptr;
   }
@@ -401,7 +405,7 @@ static int upload_blocks(mmb_engine* e) {
     d.width = (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) ? h.width : nullptr;
     d.sigl = h.sigl_d;
     d.t_sigma = h.sigma; d.t_accept = h.accept; d.t_m = h.m; d.t_flags = h.flags;
-    d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_nuts = h.nuts;
+    d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_nuts = h.nuts; d.t_nfr = h.nfr;
   }
   if (!e->d_blocks) HIPCHK(e, hipMalloc(&e->d_blocks, MMB_MAX_BLOCKS * sizeof(DBlock)));
   HIPCHK(e, hipMemcpy(e->d_blocks, db.data(), db.size() * sizeof(DBlock), hipMemcpyHostToDevice));
@@ -456,6 +460,11 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
       HIPCHK(e, hipMemcpy(h.piv, pv.data(), pv.size(), hipMemcpyHostToDevice));
       HIPCHK(e, dalloc(&h.sigl_d, (size_t)h.d * h.d));
       HIPCHK(e, hipMemcpy(h.sigl_d, h.sigl.data(), h.sigl.size() * sizeof(double), hipMemcpyHostToDevice));
+    } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
+      HIPCHK(e, dalloc(&h.nuts, K * 8));
+      HIPCHK(e, hipMemset(h.nuts, 0, K * 8 * sizeof(double)));
+      const size_t fr = (size_t)NutsFrames<Mdl<MMB_MODEL_LINE>::G * Mdl<MMB_MODEL_LINE>::R>::DBL;
+      HIPCHK(e, dalloc(&h.nfr, K * fr));
     } else if (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) {
       HIPCHK(e, dalloc(&h.width, h.tuning.size()));
       HIPCHK(e, hipMemcpy(h.width, h.tuning.data(), h.tuning.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -640,6 +649,16 @@ int mmb_get_tune(mmb_engine* e, double* tune) {
         p += h.T;
         for (int i = 0; i < h.d; ++i) p[i] = pv[k * DP + i];
       }
+    } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
+      std::vector<double> nt;
+      if ((rc = d2h(e, nt, h.nuts, K * 8))) return rc;
+      for (int64_t k = 0; k < K; ++k) {  // [adapt, m, eps, epsbar, Hbar, mu, alpha, nalpha, init]
+        double* t = tune + k * TL + off;
+        t[0] = (fl[k] & 1) ? 1.0 : 0.0;
+        t[1] = m[k];
+        for (int i = 0; i < 6; ++i) t[2 + i] = nt[k * 8 + i];
+        t[8] = (fl[k] & 8) ? 1.0 : 0.0;
+      }
     }
     off += h.tune_len;
   }
@@ -685,6 +704,15 @@ int mmb_set_tune(mmb_engine* e, const double* tune) {
       if ((rc = h2d(e, h.Mv, mv)) || (rc = h2d(e, h.Mvv, mvv)) || (rc = h2d(e, h.Ls, ls)) ||
           (rc = h2d(e, h.piv, pv)))
         return rc;
+    } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
+      std::vector<double> nt(K * 8, 0.0);
+      for (int64_t k = 0; k < K; ++k) {
+        const double* t = tune + k * TL + off;
+        fl[k] = (t[0] != 0.0 ? 1 : 0) | (t[8] != 0.0 ? 8 : 0);
+        m[k] = (int32_t)t[1];
+        for (int i = 0; i < 6; ++i) nt[k * 8 + i] = t[2 + i];
+      }
+      if ((rc = h2d(e, h.nuts, nt))) return rc;
     }
     if ((rc = h2d(e, h.m, m)) || (rc = h2d(e, h.flags, fl))) return rc;
     off += h.tune_len;

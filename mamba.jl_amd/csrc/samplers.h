@@ -4,6 +4,7 @@
 // is mirrored draw for draw by oracle/oracle.c.
 #pragma once
 #include "models.h"
+#include "nuts.h"
 
 template <class M>
 struct Smp {
@@ -524,5 +525,40 @@ struct Smp {
       k += (uint32_t)d;
     }
     M::relist(B, s, g, x);
+  }
+
+  // ---------------------------------------------------------------- NUTS
+  // sample!(v::NUTSVariate) with the model gradient computed inline (nuts.h machine).
+  // Model path: adapts iff iter <= burnin (nuts.jl:52).
+  __device__ __forceinline__ static void nuts(const SweepArgs& A, const DBlock& B, int c, int64_t it, int b,
+                                              St& s, const Grp<G>& g) {
+    using NU = Nuts<G, R>;
+    typename NU::St S;
+    const double* tn = B.t_nuts + (size_t)c * 8;
+    S.t_eps = tn[0]; S.t_epsbar = tn[1]; S.t_Hbar = tn[2]; S.t_mu = tn[3];
+    S.t_alpha = tn[4]; S.t_nalpha = tn[5];
+    S.t_m = B.t_m[c];
+    S.t_flags = B.t_flags[c];
+    M::unlist(B, s, g.lane, S.v);
+    S.pc = NPC_BEGIN;
+    const uint32_t chain = A.chain_offset + (uint32_t)c;
+    typename NU::Env E;
+    E.d = B.d;
+    E.lane = g.lane;
+    E.adapt = it <= A.model_burnin;
+    E.target = B.target;
+    E.rn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_NORMAL);
+    E.ru = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_UNIFORM);
+    E.ri = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_INIT);
+    E.F = B.t_nfr + (size_t)c * NutsFrames<NU::DV>::DBL;
+    while (NU::advance(S, E, g)) S.lf = M::logf_grad(A, B, s, S.x, S.g);
+    double* tw = B.t_nuts + (size_t)c * 8;
+    if (g.lane == 0) {
+      tw[0] = S.t_eps; tw[1] = S.t_epsbar; tw[2] = S.t_Hbar; tw[3] = S.t_mu;
+      tw[4] = S.t_alpha; tw[5] = S.t_nalpha;
+      B.t_m[c] = S.t_m;
+      B.t_flags[c] = S.t_flags;
+    }
+    M::relist(B, s, g, S.v);
   }
 };

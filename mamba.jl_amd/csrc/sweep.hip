@@ -50,6 +50,9 @@ __global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const Sweep
             else S::slice_multi(A, B, ru, s, l, g);
           }
           break;
+        case MMB_SAMPLER_NUTS:
+          if constexpr ((KINDS >> MMB_SAMPLER_NUTS) & 1u) S::nuts(A, B, c, it, b, s, g);
+          break;
         case MMB_SAMPLER_GIBBS: if constexpr ((KINDS >> MMB_SAMPLER_GIBBS) & 1u) {
           const mmb_rng gn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_N);
           const mmb_rng gu = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_U);
@@ -73,6 +76,7 @@ __global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const Sweep
 
 constexpr unsigned K_ALL = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_AMM) |
                          (1u << MMB_SAMPLER_SLICE) | (1u << MMB_SAMPLER_GIBBS);
+constexpr unsigned K_ALL_NUTS = K_ALL | (1u << MMB_SAMPLER_NUTS);
 constexpr unsigned K_GIBBS_AMM = (1u << MMB_SAMPLER_AMM) | (1u << MMB_SAMPLER_GIBBS);
 constexpr unsigned K_SLICE_AMWG = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_SLICE);
 
@@ -93,6 +97,9 @@ hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipSt
     if ((kinds & ~K_SLICE_AMWG) == 0) return launch<MMB_MODEL_RATS, K_SLICE_AMWG>(A, st, 256);
     return launch<MMB_MODEL_RATS, K_ALL>(A, st, 256);
   }
-  if (model == MMB_MODEL_LINE) return launch<MMB_MODEL_LINE, K_ALL>(A, st, 64);
+  if (model == MMB_MODEL_LINE) {
+    if (kinds & (1u << MMB_SAMPLER_NUTS)) return launch<MMB_MODEL_LINE, K_ALL_NUTS>(A, st, 64);
+    return launch<MMB_MODEL_LINE, K_ALL>(A, st, 64);
+  }
   return hipErrorInvalidValue;
 }

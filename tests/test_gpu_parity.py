@@ -41,6 +41,8 @@ LINE_SCHEMES = {
     "slice_multi": lambda M: [M.Slice(["beta", "s2"], 2.0)],
     "gibbs": lambda M: [M.Gibbs("beta"), M.Gibbs("s2")],
     "amwg_slice": lambda M: [M.AMWG("beta", 1.0), M.Slice("s2", 3.0, transform=True)],
+    "nuts": lambda M: [M.NUTS(["beta", "s2"])],
+    "nuts_slice": lambda M: [M.NUTS("beta"), M.Slice("s2", 3.0)],        # doc/tutorial/line.jl:53-56
 }
 
 
