@@ -17,8 +17,11 @@
 #include "device.h"
 #include "models.h"
 #include "nuts.h"
+#include "logistic.h"
 
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
+hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st);
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
                                hipStream_t st);
 hipError_t mmb_launch_gr_stats(int pmon, int64_t n, int K, const double* draws, const int32_t* link,
@@ -57,6 +60,14 @@ struct mmb_engine {
   int64_t iter = 0;
   double* d_vals = nullptr;
   DBlock* d_blocks = nullptr;
+  // logistic (config 4): padded X/y and the NUTS machine state (logistic.h)
+  int lg_N = 0, lg_p = 0, lg_rpr = 0;
+  double *lg_X = nullptr, *lg_y = nullptr;
+  double *lg_vec = nullptr, *lg_sc = nullptr, *lg_frames = nullptr, *lg_pos = nullptr;
+  double *lg_gpart = nullptr, *lg_lpart = nullptr;
+  int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr;
+  int64_t* lg_itc = nullptr;
+  int64_t lg_steps = 0;  // gradient steps of the last window
   // draws of the last window
   double* d_draws = nullptr;
   size_t draws_cap = 0;
@@ -156,8 +167,16 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
     e->P = 3; e->pmon = 3; e->VS = Mdl<MMB_MODEL_LINE>::VS;
     e->DP = Mdl<MMB_MODEL_LINE>::DP; e->TP = Mdl<MMB_MODEL_LINE>::TP;
   } else if (e->model == MMB_MODEL_LOGISTIC) {
-    delete e;
-    return fail(nullptr, MMB_E_UNSUPPORTED, "logistic model: NUTS engine not built in this version");
+    if (spec->ncoef < 1 || spec->ncoef > MMB_LG_DV || spec->nobs < 1 || !(spec->prior_sd > 0.0)) {
+      delete e;
+      return fail(nullptr, MMB_E_ARG, "logistic: need 1 <= ncoef <= %d, nobs >= 1, prior_sd > 0", MMB_LG_DV);
+    }
+    if (spec->nblocks != 1 || spec->blocks[0].sampler != MMB_SAMPLER_NUTS) {
+      delete e;
+      return fail(nullptr, MMB_E_UNSUPPORTED, "logistic: only the [NUTS(:beta)] scheme is lowered");
+    }
+    e->P = spec->ncoef; e->pmon = spec->ncoef; e->VS = MMB_LG_DV; e->DP = MMB_LG_DV; e->TP = 0;
+    e->lg_N = spec->nobs; e->lg_p = spec->ncoef; e->lg_rpr = mmb_lg_rpr(spec->nobs);
   } else {
     delete e;
     return fail(nullptr, MMB_E_UNSUPPORTED, "unknown model kind %d", spec->model);
@@ -272,6 +291,15 @@ static void free_dev(mmb_engine* e) {
   }
   if (e->d_vals) (void)hipFree(e->d_vals);
   if (e->d_blocks) (void)hipFree(e->d_blocks);
+  {
+    void* lp[] = {e->lg_vec, e->lg_sc, e->lg_frames, e->lg_pos, e->lg_gpart, e->lg_lpart, e->lg_iv,
+                  e->lg_count, e->lg_itc};
+    for (void* q : lp)
+      if (q) (void)hipFree(q);
+    e->lg_vec = e->lg_sc = e->lg_frames = e->lg_pos = e->lg_gpart = e->lg_lpart = nullptr;
+    e->lg_iv = e->lg_count = nullptr;
+    e->lg_itc = nullptr;
+  }
   if (e->d_draws) (void)hipFree(e->d_draws);
   e->d_vals = nullptr;
   e->d_blocks = nullptr;
@@ -285,6 +313,9 @@ void mmb_destroy(mmb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   free_dev(e);
   if (e->d_data) (void)hipFree(e->d_data);
+  if (e->lg_X) (void)hipFree(e->lg_X);
+  if (e->lg_y) (void)hipFree(e->lg_y);
+  if (e->lg_hcount) (void)hipHostFree(e->lg_hcount);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
@@ -300,6 +331,33 @@ int mmb_set_data(mmb_engine* e, const char* name, const double* x, int64_t n) {
     if (nm == "x") e->x.assign(x, x + 5);
     else if (nm == "y") e->y.assign(x, x + 5);
     else return fail(e, MMB_E_ARG, "line: unknown input %s", name);
+  } else if (e->model == MMB_MODEL_LOGISTIC) {
+    if (nm == "X") {
+      if (n != (int64_t)e->lg_N * e->lg_p) return fail(e, MMB_E_ARG, "logistic: X must be nobs x ncoef");
+      e->X.assign(x, x + n);
+    } else if (nm == "y") {
+      if (n != e->lg_N) return fail(e, MMB_E_ARG, "logistic: y must have nobs elements");
+      for (int64_t i = 0; i < n; ++i)
+        if (!(x[i] == 0.0 || x[i] == 1.0)) return fail(e, MMB_E_ARG, "logistic: y must be 0/1");
+      e->y.assign(x, x + n);
+    } else {
+      return fail(e, MMB_E_ARG, "logistic: unknown input %s", name);
+    }
+    e->have_data = !e->X.empty() && !e->y.empty();
+    if (e->have_data) {  // padded device copies: [N_pad][64], N_pad = MMB_LG_NR * rows per range
+      const size_t Np = (size_t)MMB_LG_NR * e->lg_rpr;
+      std::vector<double> hx(Np * MMB_LG_DV, 0.0), hy(Np, 0.0);
+      for (int i = 0; i < e->lg_N; ++i) {
+        for (int k = 0; k < e->lg_p; ++k) hx[(size_t)i * MMB_LG_DV + k] = e->X[(size_t)i * e->lg_p + k];
+        hy[i] = e->y[i];
+      }
+      HIPCHK(e, hipSetDevice(e->device));
+      if (!e->lg_X) HIPCHK(e, hipMalloc(&e->lg_X, hx.size() * sizeof(double)));
+      if (!e->lg_y) HIPCHK(e, hipMalloc(&e->lg_y, hy.size() * sizeof(double)));
+      HIPCHK(e, hipMemcpy(e->lg_X, hx.data(), hx.size() * sizeof(double), hipMemcpyHostToDevice));
+      HIPCHK(e, hipMemcpy(e->lg_y, hy.data(), hy.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    return 0;
   } else if (e->model == MMB_MODEL_RATS) {
     if (nm == "y") {
       if (n != 150) return fail(e, MMB_E_ARG, "rats: y must have 150 elements");
@@ -338,6 +396,9 @@ static void to_device_layout(const mmb_engine* e, const double* v, double* dv) {
     std::fill(dv, dv + e->VS, 0.0);
     for (int i = 0; i < 30; ++i) { dv[i] = v[1 + i]; dv[32 + i] = v[33 + i]; }
     dv[64] = v[0]; dv[65] = v[31]; dv[66] = v[32]; dv[67] = v[63]; dv[68] = v[64];
+  } else if (e->model == MMB_MODEL_LOGISTIC) {
+    std::fill(dv, dv + e->VS, 0.0);
+    for (int i = 0; i < e->P; ++i) dv[i] = v[i];
   } else {
     dv[0] = v[0]; dv[1] = v[1]; dv[2] = v[2]; dv[3] = 0.0;
   }
@@ -346,6 +407,8 @@ static void from_device_layout(const mmb_engine* e, const double* dv, double* v)
   if (e->model == MMB_MODEL_RATS) {
     for (int i = 0; i < 30; ++i) { v[1 + i] = dv[i]; v[33 + i] = dv[32 + i]; }
     v[0] = dv[64]; v[31] = dv[65]; v[32] = dv[66]; v[63] = dv[67]; v[64] = dv[68];
+  } else if (e->model == MMB_MODEL_LOGISTIC) {
+    for (int i = 0; i < e->P; ++i) v[i] = dv[i];
   } else {
     v[0] = dv[0]; v[1] = dv[1]; v[2] = dv[2];
   }
@@ -463,12 +526,28 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
       HIPCHK(e, dalloc(&h.nuts, K * 8));
       HIPCHK(e, hipMemset(h.nuts, 0, K * 8 * sizeof(double)));
-      const size_t fr = (size_t)NutsFrames<Mdl<MMB_MODEL_LINE>::G * Mdl<MMB_MODEL_LINE>::R>::DBL;
-      HIPCHK(e, dalloc(&h.nfr, K * fr));
+      if (e->model == MMB_MODEL_LINE) {
+        const size_t fr = (size_t)NutsFrames<Mdl<MMB_MODEL_LINE>::G * Mdl<MMB_MODEL_LINE>::R>::DBL;
+        HIPCHK(e, dalloc(&h.nfr, K * fr));
+      }
     } else if (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) {
       HIPCHK(e, dalloc(&h.width, h.tuning.size()));
       HIPCHK(e, hipMemcpy(h.width, h.tuning.data(), h.tuning.size() * sizeof(double), hipMemcpyHostToDevice));
     }
+  }
+  if (e->model == MMB_MODEL_LOGISTIC) {
+    HIPCHK(e, dalloc(&e->lg_vec, (size_t)K * MMB_LG_NVEC * MMB_LG_DV));
+    HIPCHK(e, hipMemset(e->lg_vec, 0, (size_t)K * MMB_LG_NVEC * MMB_LG_DV * sizeof(double)));
+    HIPCHK(e, dalloc(&e->lg_sc, (size_t)K * MMB_LG_NSC));
+    HIPCHK(e, dalloc(&e->lg_iv, (size_t)K * MMB_LG_NIV));
+    HIPCHK(e, hipMemset(e->lg_iv, 0, (size_t)K * MMB_LG_NIV * sizeof(int32_t)));
+    HIPCHK(e, dalloc(&e->lg_itc, (size_t)K));
+    HIPCHK(e, dalloc(&e->lg_frames, (size_t)K * NutsFrames<MMB_LG_DV>::DBL));
+    HIPCHK(e, dalloc(&e->lg_pos, (size_t)K * MMB_LG_DV));
+    HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NR * K * MMB_LG_DV));
+    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NR * K));
+    HIPCHK(e, dalloc(&e->lg_count, 2));
+    if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, sizeof(int32_t), 0));
   }
   int rc = upload_blocks(e);
   if (rc) return rc;
@@ -505,6 +584,92 @@ static int iters_per_launch(const mmb_engine* e) {
   return e->model == MMB_MODEL_RATS ? 8 : 64;
 }
 
+// Config-4 window: ctl / grad kernel pairs until no chain requests a gradient.  The
+// request count is read back every LG_CHECK steps (pinned host word); surplus pairs after
+// the last chain finished are no-ops (the grad kernel exits on count 0, idle chains return).
+static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int64_t kept0, int64_t nk,
+                        bool want) {
+  constexpr int LG_CHECK = 8;
+  const BlockHost& h = e->blocks[0];
+  LgArgs A;
+  std::memset(&A, 0, sizeof A);
+  A.K = (int32_t)e->K; A.p = e->lg_p; A.N = e->lg_N; A.rpr = e->lg_rpr;
+  A.chain_offset = (uint32_t)e->chain_offset;
+  A.seed = e->seed;
+  A.iter0 = e->iter;
+  A.it_end = e->iter + a->iters;
+  A.burnin = a->burnin; A.thin = a->thin; A.model_burnin = a->model_burnin; A.kept_origin = kept0;
+  A.prior_sd = e->spec.prior_sd;
+  A.target = h.spec.target;
+  A.X = e->lg_X; A.y = e->lg_y;
+  A.vals = e->d_vals; A.vec = e->lg_vec; A.sc = e->lg_sc; A.iv = e->lg_iv; A.itc = e->lg_itc;
+  A.frames = e->lg_frames; A.tune = h.nuts; A.tm = h.m; A.tflags = h.flags;
+  A.draws = draws;
+  A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count;
+  e->kernel_ms = 0.0;
+  e->launches = 0;
+  e->units = 0;
+  e->lg_steps = 0;
+  if (a->iters > 0) {
+    // every update needs >= 1 gradient; a tree has <= 2^depth leaves; nutsepsilon <= 4001
+    const int64_t cap = a->iters * ((1LL << MMB_NUTS_MAX_DEPTH) + 2) + 4002 + 4 * LG_CHECK;
+    std::vector<hipEvent_t>& ev = e->evpool;
+    HIPCHK(e, hipMemsetAsync(e->lg_count, 0, 2 * sizeof(int32_t), e->stream));
+    hipError_t st = mmb_lg_launch_ctl(A, 1, 0, e->stream);
+    if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
+    int64_t s = 0;
+    for (;;) {
+      const int par = (int)(s & 1);
+      if (a->time_kernels) {
+        while ((int64_t)ev.size() < 2 * (s + 1)) {
+          hipEvent_t x;
+          HIPCHK(e, hipEventCreate(&x));
+          ev.push_back(x);
+        }
+        HIPCHK(e, hipEventRecord(ev[2 * s], e->stream));
+      }
+      st = mmb_lg_launch_grad(A, par, e->stream);
+      if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_grad launch: %s", hipGetErrorString(st));
+      if (a->time_kernels) HIPCHK(e, hipEventRecord(ev[2 * s + 1], e->stream));
+      st = mmb_lg_launch_ctl(A, 0, par ^ 1, e->stream);
+      if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
+      ++s;
+      if (s % LG_CHECK == 0) {
+        HIPCHK(e, hipMemcpyAsync(e->lg_hcount, e->lg_count + (s & 1), sizeof(int32_t), hipMemcpyDeviceToHost,
+                                 e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (*e->lg_hcount == 0) break;
+      }
+      if (s > cap) return fail(e, MMB_E_STATE, "logistic NUTS window did not terminate");
+    }
+    e->lg_steps = s;
+    if (a->time_kernels) {
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      for (int64_t i = 0; i < s; ++i) {
+        float ms = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+        e->kernel_ms += ms;
+      }
+    }
+    e->launches = s;
+    e->units = a->iters * e->K;
+  }
+  e->iter += a->iters;
+  e->n_kept = want ? nk : 0;
+  if (a->draws && nk > 0) {
+    std::vector<double> hd((size_t)nk * e->pmon * e->K);
+    HIPCHK(e, hipMemcpyAsync(hd.data(), e->d_draws, hd.size() * sizeof(double), hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    for (int64_t i = 0; i < nk; ++i)
+      for (int j = 0; j < e->pmon; ++j)
+        for (int64_t k = 0; k < e->K; ++k)
+          a->draws[i + nk * (j + (int64_t)e->pmon * k)] = hd[(i * e->pmon + j) * e->K + k];
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return 0;
+}
+
 int mmb_run(mmb_engine* e, const mmb_run_args* a) {
   if (!e || !a) return fail(e, MMB_E_ARG, "null argument");
   if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
@@ -525,6 +690,7 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
       e->draws_cap = need;
     }
   }
+  if (e->model == MMB_MODEL_LOGISTIC) return run_logistic(e, a, (want && nk > 0) ? e->d_draws : nullptr, kept0, nk, want);
   SweepArgs A;
   fill_args(e, A);
   A.burnin = a->burnin;
@@ -729,6 +895,7 @@ int64_t mmb_gr_len(const mmb_engine* e) {
 
 int mmb_gr_range(mmb_engine* e, double* minmax) {
   if (!e || !minmax) return fail(e, MMB_E_ARG, "null argument");
+  if (e->pmon > 4) return fail(e, MMB_E_UNSUPPORTED, "device Gelman-Rubin supports <= 4 monitored values");
   if (e->n_kept < 1) return fail(e, MMB_E_STATE, "no device-kept draws (run with keep_device=1)");
   HIPCHK(e, hipSetDevice(e->device));
   double* d = nullptr;
@@ -743,6 +910,7 @@ int mmb_gr_range(mmb_engine* e, double* minmax) {
 
 int mmb_gr_partials(mmb_engine* e, const int32_t* link, const double* shift, double* out) {
   if (!e || !link || !shift || !out) return fail(e, MMB_E_ARG, "null argument");
+  if (e->pmon > 4) return fail(e, MMB_E_UNSUPPORTED, "device Gelman-Rubin supports <= 4 monitored values");
   if (e->n_kept < 2) return fail(e, MMB_E_STATE, "need >= 2 device-kept draws per chain");
   HIPCHK(e, hipSetDevice(e->device));
   const int p = e->pmon;

@@ -1,0 +1,42 @@
+// logistic.h — device state of the batched-gradient NUTS engine (BASELINE config 4).
+//
+// Model (build-defined after doc/examples/surgical.jl:14-24):
+//   y[n] ~ Bernoulli(invlogit(X[n,:] beta)),  beta ~ MvNormal(p, prior_sd),  scheme [NUTS(:beta)].
+// One wave per chain runs the NUTS machine of nuts.h (lane e <-> beta[e], p <= 64) in
+// lg_ctl_kernel until every chain either needs logf/grad at its leapfrog position or has
+// finished the window; lg_grad_kernel then evaluates all requested gradients at once as
+// two f64 MFMA GEMMs, X * B and X' * R, with the residual nonlinearity fused in between.
+#pragma once
+#include <stdint.h>
+
+#include "mmb_math.h"
+
+#define MMB_LG_NVEC 12  // machine vectors kept per chain besides v (nuts.h NutsM order)
+#define MMB_LG_NSC 16
+#define MMB_LG_NIV 16
+
+struct LgArgs {
+  int32_t K, p, N, rpr;    // chains, coefficients, rows, rows per range (mmb_lg_rpr)
+  uint32_t chain_offset;
+  uint64_t seed;
+  int64_t iter0, it_end;   // window = iter0+1 .. it_end
+  int64_t burnin, thin, model_burnin, kept_origin;
+  double prior_sd, target;
+  const double* X;         // [N_pad][64] row-major, zero padded (rows and columns)
+  const double* y;         // [N_pad]
+  double* vals;            // [K][64] beta (the NUTS variate v)
+  double* vec;             // [K][MMB_LG_NVEC][64]
+  double* sc;              // [K][MMB_LG_NSC]
+  int32_t* iv;             // [K][MMB_LG_NIV]
+  int64_t* itc;            // [K] last completed iteration
+  double* frames;          // [K][NutsFrames<64>::DBL]
+  double* tune;            // [K][8] eps, epsbar, Hbar, mu, alpha, nalpha
+  int32_t* tm;             // [K] m
+  int32_t* tflags;         // [K]
+  double* draws;           // [n_kept][p][K] or null
+  // gradient exchange between the two kernels
+  double* pos;             // [K][64] positions of the chains that requested a gradient (slot order)
+  double* gpart;           // [MMB_LG_NR][K][64]
+  double* lpart;           // [MMB_LG_NR][K]
+  int32_t* count;          // [2] requests in the current step (ping-pong by step parity)
+};

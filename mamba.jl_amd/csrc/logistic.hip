@@ -1,0 +1,194 @@
+// logistic.hip — NUTS on the logistic model with batched MFMA gradients (config 4).
+//
+// Step s of a window: lg_ctl_kernel(parity = s & 1) advances every chain's NUTS machine
+// (nuts.h) to its next gradient request, appending the chain's leapfrog position to
+// pos[slot] (slot = atomic counter; a chain's arithmetic does not depend on its slot);
+// lg_grad_kernel(parity) evaluates, for all requested slots,
+//   eta = X * B                      (N x 64)·(64 x slots), f64 MFMA 16x16x4
+//   lp  = y .* eta - softplus(eta),  res = y - invlogit(eta)      (fused, registers)
+//   G   = X' * res                   (64 x N)·(N x slots), f64 MFMA, D regs of the first
+//                                    GEMM reused directly as B operands of the second
+// as MMB_LG_NR row-range partials; the next lg_ctl_kernel sums the partials in range order
+// (no atomics: the summation order is fixed and restated by oracle/oracle.c).
+#include "logistic.h"
+#include "nuts.h"
+
+typedef double mmb_d4 __attribute__((ext_vector_type(4)));
+
+using NU = Nuts<64, 1>;
+using LgFr = NutsFrames<64>;
+
+__device__ __forceinline__ static void lg_load(const LgArgs& A, int c, int lane, NU::St& S) {
+  const double* vb = A.vec + (size_t)c * MMB_LG_NVEC * 64 + lane;
+  S.x[0] = vb[0 * 64]; S.r[0] = vb[1 * 64]; S.g[0] = vb[2 * 64];
+  S.xm[0] = vb[3 * 64]; S.rm[0] = vb[4 * 64]; S.gm[0] = vb[5 * 64];
+  S.xp[0] = vb[6 * 64]; S.rp[0] = vb[7 * 64]; S.gp[0] = vb[8 * 64];
+  S.r0[0] = vb[9 * 64]; S.g0[0] = vb[10 * 64]; S.cxp[0] = vb[11 * 64];
+  S.v[0] = A.vals[(size_t)c * 64 + lane];
+  const double* s = A.sc + (size_t)c * MMB_LG_NSC;
+  S.logp0 = s[0]; S.logu0 = s[1]; S.n = s[2]; S.cn = s[3]; S.calpha = s[4]; S.cnalpha = s[5];
+  S.eps = s[6]; S.logf0 = s[7]; S.prob = s[8];
+  const int32_t* iv = A.iv + (size_t)c * MMB_LG_NIV;
+  S.pc = iv[0]; S.j = iv[1]; S.l = iv[2]; S.nxt = iv[3]; S.ku = iv[4]; S.pm = iv[5]; S.s = iv[6];
+  S.cs = iv[7]; S.phases = iv[8]; S.eit = iv[9];
+  const double* t = A.tune + (size_t)c * 8;
+  S.t_eps = t[0]; S.t_epsbar = t[1]; S.t_Hbar = t[2]; S.t_mu = t[3]; S.t_alpha = t[4]; S.t_nalpha = t[5];
+  S.t_m = A.tm[c];
+  S.t_flags = A.tflags[c];
+}
+
+__device__ __forceinline__ static void lg_store(const LgArgs& A, int c, int lane, const NU::St& S, int slot,
+                                                int64_t itc) {
+  double* vb = A.vec + (size_t)c * MMB_LG_NVEC * 64 + lane;
+  vb[0 * 64] = S.x[0]; vb[1 * 64] = S.r[0]; vb[2 * 64] = S.g[0];
+  vb[3 * 64] = S.xm[0]; vb[4 * 64] = S.rm[0]; vb[5 * 64] = S.gm[0];
+  vb[6 * 64] = S.xp[0]; vb[7 * 64] = S.rp[0]; vb[8 * 64] = S.gp[0];
+  vb[9 * 64] = S.r0[0]; vb[10 * 64] = S.g0[0]; vb[11 * 64] = S.cxp[0];
+  A.vals[(size_t)c * 64 + lane] = S.v[0];
+  if (lane == 0) {
+    double* s = A.sc + (size_t)c * MMB_LG_NSC;
+    s[0] = S.logp0; s[1] = S.logu0; s[2] = S.n; s[3] = S.cn; s[4] = S.calpha; s[5] = S.cnalpha;
+    s[6] = S.eps; s[7] = S.logf0; s[8] = S.prob;
+    int32_t* iv = A.iv + (size_t)c * MMB_LG_NIV;
+    iv[0] = S.pc; iv[1] = S.j; iv[2] = S.l; iv[3] = S.nxt; iv[4] = S.ku; iv[5] = S.pm; iv[6] = S.s;
+    iv[7] = S.cs; iv[8] = S.phases; iv[9] = S.eit; iv[10] = slot;
+    double* t = A.tune + (size_t)c * 8;
+    t[0] = S.t_eps; t[1] = S.t_epsbar; t[2] = S.t_Hbar; t[3] = S.t_mu; t[4] = S.t_alpha; t[5] = S.t_nalpha;
+    A.tm[c] = S.t_m;
+    A.tflags[c] = S.t_flags;
+    A.itc[c] = itc;
+  }
+}
+
+// logpdf!(m, x, block) and its gradient at S.x from the range partials (oracle logf_grad):
+// lf = 0 + prior, + sum of range partials if finite; grad = -x/sd^2 + partials, non-finite -> 0.
+__device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, int lane, const Grp<64>& g,
+                                                   NU::St& S) {
+  const bool el = lane < A.p;
+  const double x = S.x[0];
+  const double sd2 = A.prior_sd * A.prior_sd;
+  double gg = el ? -x / sd2 : 0.0;
+#pragma unroll 4
+  for (int rg = 0; rg < MMB_LG_NR; ++rg) gg = gg + A.gpart[((size_t)rg * A.K + slot) * 64 + lane];
+  if (!isfinite(gg)) gg = 0.0;
+  S.g[0] = el ? gg : 0.0;
+  const bool bad = el && !isfinite(x);
+  double sq = el ? 0.0 + x * x : 0.0;
+  const double ssq = g.sum(sq);
+  double lf = 0.0 + (__ballot(bad) ? -__builtin_inf() : d_iso(A.p, A.prior_sd, ssq));
+  if (isfinite(lf)) {
+    double ylp = 0.0;
+    for (int rg = 0; rg < MMB_LG_NR; ++rg) ylp = ylp + A.lpart[(size_t)rg * A.K + slot];
+    lf = lf + ylp;
+  }
+  S.lf = lf;
+}
+
+__global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.count[parity ^ 1] = 0;  // next step's counter
+  const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (c >= A.K) return;
+  Grp<64> g;
+  const int lane = g.lane;
+  NU::St S;
+  lg_load(A, c, lane, S);
+  int64_t itc = A.itc[c];
+  if (start) {
+    S.pc = NPC_BEGIN;
+    itc = A.iter0;
+  }
+  if (S.pc == NPC_IDLE) return;
+  if (npc_wants_grad(S.pc)) lg_assemble(A, A.iv[(size_t)c * MMB_LG_NIV + 10], lane, g, S);
+  const uint32_t chain = A.chain_offset + (uint32_t)c;
+  for (;;) {
+    const int64_t cur = itc + 1;
+    NU::Env E;
+    E.d = A.p;
+    E.lane = lane;
+    E.adapt = cur <= A.model_burnin;
+    E.target = A.target;
+    E.rn = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_NORMAL);
+    E.ru = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_UNIFORM);
+    E.ri = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_INIT);
+    E.F = A.frames + (size_t)c * LgFr::DBL;
+    if (NU::advance(S, E, g)) {
+      int slot = 0;
+      if (lane == 0) slot = atomicAdd(&A.count[parity], 1);
+      slot = __shfl(slot, 0, 64);
+      A.pos[(size_t)slot * 64 + lane] = S.x[0];
+      lg_store(A, c, lane, S, slot, itc);
+      return;
+    }
+    itc = cur;  // mcmc_worker! keep rule (mcmc.jl:76): sim[i,:,1] = unlist(m, true)
+    if (A.draws && itc > A.burnin && (itc - A.burnin) % A.thin == 0 && lane < A.p) {
+      const int64_t row = (itc - A.burnin) / A.thin - 1 - A.kept_origin;
+      A.draws[(size_t)(row * A.p + lane) * A.K + c] = S.v[0];
+    }
+    if (itc >= A.it_end) {
+      S.pc = NPC_IDLE;
+      lg_store(A, c, lane, S, 0, itc);
+      return;
+    }
+    S.pc = NPC_BEGIN;
+  }
+}
+
+// grid (ceil(K/64), MMB_LG_NR), 256 threads: wave w handles slots [64*bx + 16*w, +16) over
+// the rows of range blockIdx.y.  Lane l: chain column l & 15, k-group l >> 4.
+__global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity) {
+  const int nact = A.count[parity];
+  if ((int)blockIdx.x * 64 >= nact) return;
+  const int l = (int)(threadIdx.x & 63);
+  const int lc = l & 15, lq = l >> 4;
+  const int slot = (int)blockIdx.x * 64 + (int)(threadIdx.x >> 6) * 16 + lc;
+  const bool live = slot < nact;
+  const int rg = (int)blockIdx.y;
+  double bpos[13];
+#pragma unroll
+  for (int kk = 0; kk < 13; ++kk) bpos[kk] = live ? A.pos[(size_t)slot * 64 + 4 * kk + lq] : 0.0;
+  mmb_d4 acc[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
+  double lsum = 0.0;
+  const int nb = A.rpr / 16;
+  for (int b = 0; b < nb; ++b) {
+    const int r0 = rg * A.rpr + 16 * b;
+    const double* xa = A.X + (size_t)(r0 + lc) * 64 + lq;
+    mmb_d4 eta = mmb_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 13; ++kk) eta = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[4 * kk], bpos[kk], eta, 0, 0, 0);
+    double s[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r0 + lq + 4 * i;
+      double lp = 0.0, res = 0.0;
+      if (row < A.N) mmb_logistic_terms(eta[i], A.y[row], &lp, &res);
+      lsum = lsum + lp;
+      s[i] = res;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double* xt = A.X + (size_t)(r0 + 4 * i + lq) * 64 + lc;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xt[16 * mt], s[i], acc[mt], 0, 0, 0);
+    }
+  }
+  lsum = lsum + __shfl_xor(lsum, 16, 64);
+  lsum = lsum + __shfl_xor(lsum, 32, 64);
+  if (!live) return;
+  if (lq == 0) A.lpart[(size_t)rg * A.K + slot] = lsum;
+  double* gp = A.gpart + ((size_t)rg * A.K + slot) * 64;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gp[16 * mt + lq + 4 * q] = acc[mt][q];
+}
+
+hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st) {
+  hipLaunchKernelGGL(lg_ctl_kernel, dim3((A.K + 3) / 4), dim3(256), 0, st, A, start, parity);
+  return hipGetLastError();
+}
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {
+  hipLaunchKernelGGL(lg_grad_kernel, dim3((A.K + 63) / 64, MMB_LG_NR), dim3(256), 0, st, A, parity);
+  return hipGetLastError();
+}

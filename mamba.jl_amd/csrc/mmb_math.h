@@ -294,4 +294,23 @@ MMB_HD double mmb_gamma_mt(double a, const mmb_rng* sn, const mmb_rng* su, uint3
   }
 }
 
+/* ---- logistic likelihood (BASELINE config 4): y ~ Bernoulli(invlogit(eta)).
+ * Per observation: log-density y*eta - softplus(eta) and score residual y - invlogit(eta),
+ * both from t = exp(-|eta|) (stable for any eta).  The batched gradient sums over rows in
+ * MMB_LG_NR fixed row ranges of mmb_lg_rpr(N) rows (a multiple of 16, the MFMA tile);
+ * the range structure is part of the summation spec that the oracle restates. */
+#define MMB_LG_NR 16
+#define MMB_LG_DV 64 /* coefficients per chain, padded (p <= 64) */
+MMB_HD int mmb_lg_rpr(int N) {
+  int per = (N + MMB_LG_NR - 1) / MMB_LG_NR;
+  return ((per + 15) / 16) * 16;
+}
+MMB_HD void mmb_logistic_terms(double eta, double y, double* lp, double* res) {
+  double t = mmb_exp(-fabs(eta));
+  double sp = (eta > 0.0 ? eta : 0.0) + mmb_log1p(t);
+  *lp = y * eta - sp;
+  double q = 1.0 / (1.0 + t);
+  *res = y - (eta >= 0.0 ? q : t * q);
+}
+
 #endif /* MMB_MATH_H */

@@ -127,3 +127,22 @@ def test_mcmc_api_and_full_size_properties(mamba):
     mb = sim["mu_beta"].mean()
     a0 = sim["alpha0"].mean()
     assert abs(mb - 6.183) < 0.02 and abs(a0 - 106.63) < 0.5, (mb, a0)
+
+
+def logistic(mamba, nobs, ncoef):
+    data, bt = mamba.model.logistic_data(nobs, ncoef)
+    m = mamba.logistic(nobs, ncoef, 10.0)
+    m.setinputs(data)
+    return m.setsamplers([mamba.NUTS("beta")]), bt
+
+
+def test_logistic_nuts_parity(mamba, oracle):
+    """Config 4 at reduced N: the batched MFMA gradient engine against the oracle's
+    sequential restatement of the same summation order."""
+    m, bt = logistic(mamba, 1000, 50)
+    K = 100                                    # 2 chain tiles, the second partly live
+    init = np.random.default_rng(8).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 30, 10, 1, model_burnin=15)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
