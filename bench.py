@@ -11,6 +11,11 @@ mmb_run window (kernels of 8 iterations); state and data are resident in HBM.
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+
+Other BASELINE configs (reported in DESIGN.md, not the metric line):
+  --workload line_amm   configs[1]: line regression, AMM, 4096 chains per GPU
+  --workload logistic   configs[3]: logistic N=10000 p=50, NUTS, 4096 chains per GPU
+                        (roofline bound "mfma": algorithmic 4*N*p flops per gradient)
 """
 import argparse
 import json
@@ -23,43 +28,53 @@ sys.path.insert(0, ROOT)
 
 CHAINS_PER_GPU = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (spec, dense)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=400)
-    p.add_argument("--warmup", type=int, default=200)
-    p.add_argument("--chains", type=int, default=CHAINS_PER_GPU, help="chains per GPU")
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=None)
+    p.add_argument("--chains", type=int, default=None, help="chains per GPU")
+    p.add_argument("--workload", default="rats", choices=["rats", "line_amm", "logistic"])
     p.add_argument("--thin", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--scheme", default="gibbs_amm",
                    help="gibbs_amm (metric config) | reference | ablations: amm_noadapt, gibbs_only")
-    return p.parse_args()
+    a = p.parse_args()
+    dflt = {"rats": (CHAINS_PER_GPU, 400, 200), "line_amm": (4096, 2000, 500), "logistic": (4096, 100, 100)}
+    k, st, wu = dflt[a.workload]
+    a.chains = a.chains or k
+    a.steps = a.steps if a.steps is not None else st
+    a.warmup = a.warmup if a.warmup is not None else wu
+    return a
 
 
-def cpu_baseline(mb, model, init, seconds):
+def cpu_baseline(mb, model, init, seconds, what="rats Gibbs+AMM sweep", per_thread=64, warm=64,
+                 model_burnin=None):
     """The CPU oracle (same algorithm, same Philox streams) on the host cores: bounded
     sample (a few thousand chain-updates per thread), OpenMP over chains."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     orc = oracle_lib.Oracle()
     threads = min(os.cpu_count() or 1, 16)
-    K = 64 * threads
+    K = min(per_thread * threads, init.shape[0])
     st = orc.new_state(model, init[:K])
-    orc.run(model, st, 64, seed=7, nthreads=threads, draws=False)  # warm (adaptation, rank)
+    orc.run(model, st, warm, seed=7, nthreads=threads, draws=False, model_burnin=model_burnin)  # warm-up
     iters, t = 16, 0.0
     while True:
         t0 = time.perf_counter()
-        orc.run(model, st, iters, burnin=0, thin=2, seed=7, nthreads=threads, draws=True)
+        orc.run(model, st, iters, burnin=0, thin=2, seed=7, nthreads=threads, draws=True,
+                model_burnin=model_burnin)
         t = time.perf_counter() - t0
         if t > seconds / 2 or iters >= 8192:
             break
         iters *= 2
     return {"value": K * iters / t, "unit": "chain-updates/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/oracle.c, {K} chains x {iters} iterations (after 64 warm-up) of the same "
-                      f"rats Gibbs+AMM sweep, OpenMP {threads} threads, {t:.1f} s"}
+            "sample": f"oracle/oracle.c, {K} chains x {iters} iterations (after {warm} warm-up) of the same "
+                      f"{what}, OpenMP {threads} threads, {t:.1f} s"}
 
 
 def scheme_for(mb, name):
@@ -77,6 +92,32 @@ def scheme_for(mb, name):
     raise SystemExit(f"unknown scheme {name}")
 
 
+def setup_workload(mb, args, rank):
+    """Model, scheme, per-chain inits and the run keywords of one BASELINE config."""
+    import numpy as np
+    K = args.chains
+    if args.workload == "rats":
+        model = mb.rats()
+        model.setinputs(mb.model.RATS_DATA)
+        model.setsamplers(scheme_for(mb, args.scheme))
+        init = mb.model.rats_init_ls(K, seed=1000 + rank)
+        desc = ("rats mixed Gibbs+AMM sweep (BASELINE configs[2]; configs[4] at N=8)"
+                if args.scheme == "gibbs_amm" else f"rats scheme {args.scheme}")
+        return model, init, desc, {"thin": args.thin}, "f64"
+    if args.workload == "line_amm":
+        model = mb.line()
+        model.setinputs(mb.model.LINE_DATA)
+        model.setsamplers([mb.AMM(["beta", "s2"], np.eye(3))])
+        init = mb.model.line_init_matrix(K, seed=1000 + rank)
+        return model, init, "line AMM (BASELINE configs[1])", {"thin": 1}, "f64"
+    data, _ = mb.model.logistic_data(10000, 50)
+    model = mb.logistic(10000, 50, 10.0)
+    model.setinputs(data)
+    model.setsamplers([mb.NUTS("beta")])
+    init = np.random.default_rng(1000 + rank).normal(0.0, 0.1, (K, 50))
+    return model, init, "logistic N=10000 p=50 NUTS (BASELINE configs[3])", {"thin": 1}, "f64"
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,13 +130,12 @@ def main():
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     import _mamba_path
     mb = _mamba_path.load()
+    import numpy as np
 
     K = args.chains
-    model = mb.rats()
-    model.setinputs(mb.model.RATS_DATA)
-    model.setsamplers(scheme_for(mb, args.scheme))
-    import numpy as np
-    init_all = mb.model.rats_init_ls(K, seed=1000 + rank)
+    model, init_all, desc, kw, dtype = setup_workload(mb, args, rank)
+    thin = kw["thin"]
+    nuts = args.workload == "logistic"
     eng = mb.Engine(model, device=local)
     eng.init_chains(init_all, chain_offset=rank * K, seed=20261015)
 
@@ -105,11 +145,13 @@ def main():
         torch.cuda.synchronize()
         eng.sync()
 
-    # warmup: adaptation reaches steady state (AMM m > 2d uses the adaptive factor)
-    eng.run(args.warmup, burnin=0, thin=args.thin, model_burnin=0, draws=False, keep_device=False)
+    # warmup: adaptation reaches steady state (AMM m > 2d uses the adaptive factor; NUTS
+    # dual averaging runs while iter <= model_burnin = warmup, then the step size is fixed)
+    mburn = args.warmup if nuts else 0
+    eng.run(args.warmup, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False)
     barrier()
     t0 = time.perf_counter()
-    eng.run(args.steps, burnin=args.warmup, thin=args.thin, model_burnin=0, draws=False, keep_device=True)
+    eng.run(args.steps, burnin=args.warmup, thin=thin, model_burnin=mburn, draws=False, keep_device=True)
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -118,42 +160,60 @@ def main():
         dt = float(t.item())
     total_units = K * world * args.steps
     value = total_units / dt
+    grads_timed = eng.grad_evals() if nuts else 0
 
-    # Gelman-Rubin over all chains of all GPUs: device partials + one RCCL all-reduce
-    def ar_sum(x):
-        if world == 1:
-            return x
-        t = torch.tensor(x, dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)
-        return t.cpu().numpy()
+    psrf = None
+    if eng.pmon <= 4:
+        # Gelman-Rubin over all chains of all GPUs: device partials + one RCCL all-reduce
+        def ar_sum(x):
+            if world == 1:
+                return x
+            t = torch.tensor(x, dtype=torch.float64, device="cuda")
+            dist.all_reduce(t)
+            return t.cpu().numpy()
 
-    def ar_minmax(lo, hi):
-        if world == 1:
-            return lo, hi
-        a = torch.tensor(np.concatenate([-lo, hi]), dtype=torch.float64, device="cuda")
-        dist.all_reduce(a, op=dist.ReduceOp.MAX)
-        a = a.cpu().numpy()
-        return -a[:len(lo)], a[len(lo):]
+        def ar_minmax(lo, hi):
+            if world == 1:
+                return lo, hi
+            a = torch.tensor(np.concatenate([-lo, hi]), dtype=torch.float64, device="cuda")
+            dist.all_reduce(a, op=dist.ReduceOp.MAX)
+            a = a.cpu().numpy()
+            return -a[:len(lo)], a[len(lo):]
 
-    psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax)
+        psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax)
 
-    # roofline: dominant kernel = the fused sweep; per-launch device time from HIP events
-    W = int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8"))
-    nroof = max(W * 8, 64)
-    eng.run(nroof, burnin=0, thin=args.thin, model_burnin=0, draws=False, keep_device=False,
-            time_kernels=True)
-    kms, launches, units = eng.kernel_time()
-    per_update = eng.state_bytes() + 8.0 * 3 / args.thin  # 2*S_state + S_draw/thin
-    bytes_per_launch = per_update * units / launches
-    avg_ms = kms / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
-    if os.path.exists(tfile):
-        try:
-            traffic = json.load(open(tfile)).get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    # roofline of the dominant kernel; per-launch device time from HIP events on the engine's stream
+    if nuts:  # lg_grad_kernel: 4*N*p algorithmic flops per gradient (X*beta and X'*res)
+        nroof = 16
+        eng.run(nroof, burnin=0, thin=1, model_burnin=mburn, draws=False, time_kernels=True)
+        kms, launches, units = eng.kernel_time()
+        flops = 4.0 * 10000 * 50 * eng.grad_evals()
+        achieved = flops / (kms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None,
+                "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": 4.0 * 10000 * 50,
+                "avg_launch_ms": kms / launches, "gradients_per_launch": eng.grad_evals() / launches,
+                "gradients_per_chain_update_timed": grads_timed / (K * args.steps)}
+    else:
+        W = int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8" if args.workload == "rats" else "64"))
+        nroof = max(W * 8, 64)
+        eng.run(nroof, burnin=0, thin=thin, model_burnin=0, draws=False, keep_device=False, time_kernels=True)
+        kms, launches, units = eng.kernel_time()
+        per_update = eng.state_bytes() + 8.0 * eng.pmon / thin  # 2*S_state + S_draw/thin
+        bytes_per_launch = per_update * units / launches
+        avg_ms = kms / launches
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+        if args.workload == "rats" and args.scheme == "gibbs_amm" and os.path.exists(tfile):
+            try:
+                traffic = json.load(open(tfile)).get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sweep_kernel",
+                "algorithmic_bytes_per_chain_update": per_update,
+                "avg_launch_ms": avg_ms, "chain_updates_per_launch": units / launches}
 
     out = {
         "metric": "chain-updates/sec (iters×chains) on rats model at 1/2/4/8 MI355X",
@@ -166,20 +226,31 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
-        "data": "rats.jl data (real, 30 rats x 5 weeks); synthetic per-chain inits (per-rat LS + jitter)",
-        "config": {"workload": "rats mixed Gibbs+AMM sweep (BASELINE configs[2]; configs[4] at N=8)"
-                   if args.scheme == "gibbs_amm" else f"rats scheme {args.scheme}",
-                   "chains_per_gpu": K, "global_chains": K * world, "thin": args.thin,
-                   "iters_per_launch": W, "amm_adapt": "all", "parallelism": f"chain-shard x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes_per_chain_update": per_update,
-                     "avg_launch_ms": avg_ms, "chain_updates_per_launch": units / launches},
-        "gelman_rubin_psrf": [float(x) for x in psrf[:, 0]],
+        "dtype": dtype,
+        "data": ("rats.jl data (real, 30 rats x 5 weeks); synthetic per-chain inits (per-rat LS + jitter)"
+                 if args.workload == "rats" else
+                 "line.jl data; synthetic inits" if args.workload == "line_amm" else
+                 "synthetic X ~ N(0,1), y ~ Bernoulli(invlogit(X beta_true)) (SURVEY §8d seeds); inits N(0, 0.1^2)"),
+        "config": {"workload": desc, "chains_per_gpu": K, "global_chains": K * world, "thin": thin,
+                   "parallelism": f"chain-shard x{world}"},
+        "roofline": roof,
     }
+    if args.workload != "rats":
+        out["metric"] = f"chain-updates/sec on {args.workload} (not the headline metric)"
+    if args.workload == "rats":
+        out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8")),
+                              "amm_adapt": "all"})
+    if psrf is not None:
+        out["gelman_rubin_psrf"] = [float(x) for x in psrf[:, 0]]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds)
+        if args.workload == "rats":
+            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds)
+        elif args.workload == "line_amm":
+            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds, "line AMM update",
+                                               per_thread=256, warm=64)
+        else:
+            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds, "logistic NUTS update",
+                                               per_thread=4, warm=20, model_burnin=20)
     if rank == 0:
         print(json.dumps(out))
     eng.close()

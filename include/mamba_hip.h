@@ -157,6 +157,9 @@ int mmb_gr_partials(mmb_engine* e, const int32_t* link_kind, const double* shift
 int mmb_sync(mmb_engine* e);
 int mmb_kernel_time(const mmb_engine* e, double* total_ms, int64_t* launches, int64_t* units);
 int mmb_state_bytes(const mmb_engine* e, double* bytes_per_chain_update);
+/* Gradient evaluations (logpdf!+gradlogpdf! calls, sampler.jl:97-119) in the last mmb_run,
+ * summed over chains; counted on device by the batched-gradient (logistic) engine, 0 else. */
+int mmb_grad_evals(mmb_engine* e, int64_t* n);
 
 #ifdef __cplusplus
 }

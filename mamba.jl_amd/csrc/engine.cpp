@@ -68,6 +68,7 @@ struct mmb_engine {
   int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr;
   int64_t* lg_itc = nullptr;
   int64_t lg_steps = 0;  // gradient steps of the last window
+  unsigned long long* lg_ngrad = nullptr;
   // draws of the last window
   double* d_draws = nullptr;
   size_t draws_cap = 0;
@@ -299,6 +300,8 @@ static void free_dev(mmb_engine* e) {
     e->lg_vec = e->lg_sc = e->lg_frames = e->lg_pos = e->lg_gpart = e->lg_lpart = nullptr;
     e->lg_iv = e->lg_count = nullptr;
     e->lg_itc = nullptr;
+    if (e->lg_ngrad) (void)hipFree(e->lg_ngrad);
+    e->lg_ngrad = nullptr;
   }
   if (e->d_draws) (void)hipFree(e->d_draws);
   e->d_vals = nullptr;
@@ -547,6 +550,7 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NR * K * MMB_LG_DV));
     HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NR * K));
     HIPCHK(e, dalloc(&e->lg_count, 2));
+    HIPCHK(e, dalloc(&e->lg_ngrad, 1));
     if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, sizeof(int32_t), 0));
   }
   int rc = upload_blocks(e);
@@ -606,6 +610,8 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.frames = e->lg_frames; A.tune = h.nuts; A.tm = h.m; A.tflags = h.flags;
   A.draws = draws;
   A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count;
+  A.ngrad = e->lg_ngrad;
+  HIPCHK(e, hipMemsetAsync(e->lg_ngrad, 0, sizeof(unsigned long long), e->stream));
   e->kernel_ms = 0.0;
   e->launches = 0;
   e->units = 0;
@@ -966,3 +972,15 @@ int mmb_state_bytes(const mmb_engine* e, double* bytes) {
   return 0;
 }
 
+
+int mmb_grad_evals(mmb_engine* e, int64_t* n) {
+  if (!e || !n) return fail(e, MMB_E_ARG, "null argument");
+  *n = 0;
+  if (e->model != MMB_MODEL_LOGISTIC || !e->lg_ngrad) return 0;
+  unsigned long long v = 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipMemcpyAsync(&v, e->lg_ngrad, sizeof v, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  *n = (int64_t)v;
+  return 0;
+}

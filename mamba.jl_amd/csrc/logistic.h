@@ -39,4 +39,5 @@ struct LgArgs {
   double* gpart;           // [MMB_LG_NR][K][64]
   double* lpart;           // [MMB_LG_NR][K]
   int32_t* count;          // [2] requests in the current step (ping-pong by step parity)
+  unsigned long long* ngrad;  // total gradient evaluations of the window
 };

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
 // the rows of range blockIdx.y.  Lane l: chain column l & 15, k-group l >> 4.
 __global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity) {
   const int nact = A.count[parity];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
   if ((int)blockIdx.x * 64 >= nact) return;
   const int l = (int)(threadIdx.x & 63);
   const int lc = l & 15, lq = l >> 4;

@@ -115,6 +115,11 @@ class Engine:
         self.lib.mmb_kernel_time(self.h, C.byref(ms), C.byref(n), C.byref(u))
         return ms.value, n.value, u.value
 
+    def grad_evals(self):
+        n = C.c_int64()
+        self._chk(self.lib.mmb_grad_evals(self.h, C.byref(n)))
+        return n.value
+
     def state_bytes(self):
         b = C.c_double()
         self.lib.mmb_state_bytes(self.h, C.byref(b))
