@@ -61,8 +61,8 @@ struct mmb_engine {
   double* d_vals = nullptr;
   DBlock* d_blocks = nullptr;
   // logistic (config 4): padded X/y and the NUTS machine state (logistic.h)
-  int lg_N = 0, lg_p = 0, lg_rpr = 0;
-  double *lg_X = nullptr, *lg_y = nullptr;
+  int lg_N = 0, lg_p = 0, lg_rps = 0;
+  double *lg_X = nullptr, *lg_Xt = nullptr, *lg_y = nullptr;
   double *lg_vec = nullptr, *lg_sc = nullptr, *lg_frames = nullptr, *lg_pos = nullptr;
   double *lg_gpart = nullptr, *lg_lpart = nullptr;
   int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr;
@@ -177,7 +177,7 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
       return fail(nullptr, MMB_E_UNSUPPORTED, "logistic: only the [NUTS(:beta)] scheme is lowered");
     }
     e->P = spec->ncoef; e->pmon = spec->ncoef; e->VS = MMB_LG_DV; e->DP = MMB_LG_DV; e->TP = 0;
-    e->lg_N = spec->nobs; e->lg_p = spec->ncoef; e->lg_rpr = mmb_lg_rpr(spec->nobs);
+    e->lg_N = spec->nobs; e->lg_p = spec->ncoef; e->lg_rps = mmb_lg_rps(spec->nobs);
   } else {
     delete e;
     return fail(nullptr, MMB_E_UNSUPPORTED, "unknown model kind %d", spec->model);
@@ -317,6 +317,7 @@ void mmb_destroy(mmb_engine* e) {
   free_dev(e);
   if (e->d_data) (void)hipFree(e->d_data);
   if (e->lg_X) (void)hipFree(e->lg_X);
+  if (e->lg_Xt) (void)hipFree(e->lg_Xt);
   if (e->lg_y) (void)hipFree(e->lg_y);
   if (e->lg_hcount) (void)hipHostFree(e->lg_hcount);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
@@ -347,17 +348,22 @@ int mmb_set_data(mmb_engine* e, const char* name, const double* x, int64_t n) {
       return fail(e, MMB_E_ARG, "logistic: unknown input %s", name);
     }
     e->have_data = !e->X.empty() && !e->y.empty();
-    if (e->have_data) {  // padded device copies: [N_pad][64], N_pad = MMB_LG_NR * rows per range
-      const size_t Np = (size_t)MMB_LG_NR * e->lg_rpr;
-      std::vector<double> hx(Np * MMB_LG_DV, 0.0), hy(Np, 0.0);
+    if (e->have_data) {  // padded device copies: X [Np][64], Xt [64][Np], y [Np]
+      const size_t Np = (size_t)MMB_LG_NG * MMB_LG_NS * e->lg_rps;
+      std::vector<double> hx(Np * MMB_LG_DV, 0.0), hxt(Np * MMB_LG_DV, 0.0), hy(Np, 0.0);
       for (int i = 0; i < e->lg_N; ++i) {
-        for (int k = 0; k < e->lg_p; ++k) hx[(size_t)i * MMB_LG_DV + k] = e->X[(size_t)i * e->lg_p + k];
+        for (int k = 0; k < e->lg_p; ++k) {
+          hx[(size_t)i * MMB_LG_DV + k] = e->X[(size_t)i * e->lg_p + k];
+          hxt[(size_t)k * Np + i] = e->X[(size_t)i * e->lg_p + k];
+        }
         hy[i] = e->y[i];
       }
       HIPCHK(e, hipSetDevice(e->device));
       if (!e->lg_X) HIPCHK(e, hipMalloc(&e->lg_X, hx.size() * sizeof(double)));
+      if (!e->lg_Xt) HIPCHK(e, hipMalloc(&e->lg_Xt, hxt.size() * sizeof(double)));
       if (!e->lg_y) HIPCHK(e, hipMalloc(&e->lg_y, hy.size() * sizeof(double)));
       HIPCHK(e, hipMemcpy(e->lg_X, hx.data(), hx.size() * sizeof(double), hipMemcpyHostToDevice));
+      HIPCHK(e, hipMemcpy(e->lg_Xt, hxt.data(), hxt.size() * sizeof(double), hipMemcpyHostToDevice));
       HIPCHK(e, hipMemcpy(e->lg_y, hy.data(), hy.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     return 0;
@@ -547,8 +553,8 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     HIPCHK(e, dalloc(&e->lg_itc, (size_t)K));
     HIPCHK(e, dalloc(&e->lg_frames, (size_t)K * NutsFrames<MMB_LG_DV>::DBL));
     HIPCHK(e, dalloc(&e->lg_pos, (size_t)K * MMB_LG_DV));
-    HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NR * K * MMB_LG_DV));
-    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NR * K));
+    HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NG * K * MMB_LG_DV));
+    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * K));
     HIPCHK(e, dalloc(&e->lg_count, 2));
     HIPCHK(e, dalloc(&e->lg_ngrad, 1));
     if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, sizeof(int32_t), 0));
@@ -597,7 +603,8 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   const BlockHost& h = e->blocks[0];
   LgArgs A;
   std::memset(&A, 0, sizeof A);
-  A.K = (int32_t)e->K; A.p = e->lg_p; A.N = e->lg_N; A.rpr = e->lg_rpr;
+  A.K = (int32_t)e->K; A.p = e->lg_p; A.N = e->lg_N; A.rps = e->lg_rps;
+  A.Np = MMB_LG_NG * MMB_LG_NS * e->lg_rps;
   A.chain_offset = (uint32_t)e->chain_offset;
   A.seed = e->seed;
   A.iter0 = e->iter;
@@ -605,7 +612,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.burnin = a->burnin; A.thin = a->thin; A.model_burnin = a->model_burnin; A.kept_origin = kept0;
   A.prior_sd = e->spec.prior_sd;
   A.target = h.spec.target;
-  A.X = e->lg_X; A.y = e->lg_y;
+  A.X = e->lg_X; A.Xt = e->lg_Xt; A.y = e->lg_y;
   A.vals = e->d_vals; A.vec = e->lg_vec; A.sc = e->lg_sc; A.iv = e->lg_iv; A.itc = e->lg_itc;
   A.frames = e->lg_frames; A.tune = h.nuts; A.tm = h.m; A.tflags = h.flags;
   A.draws = draws;

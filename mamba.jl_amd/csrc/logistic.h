@@ -16,13 +16,15 @@
 #define MMB_LG_NIV 16
 
 struct LgArgs {
-  int32_t K, p, N, rpr;    // chains, coefficients, rows, rows per range (mmb_lg_rpr)
+  int32_t K, p, N, rps;    // chains, coefficients, rows, rows per sub-range (mmb_lg_rps)
+  int32_t Np;              // padded rows = MMB_LG_NG * MMB_LG_NS * rps
   uint32_t chain_offset;
   uint64_t seed;
   int64_t iter0, it_end;   // window = iter0+1 .. it_end
   int64_t burnin, thin, model_burnin, kept_origin;
   double prior_sd, target;
-  const double* X;         // [N_pad][64] row-major, zero padded (rows and columns)
+  const double* X;         // [Np][64] row-major, zero padded (rows and columns)
+  const double* Xt;        // [64][Np] transposed copy (A operand of X * B)
   const double* y;         // [N_pad]
   double* vals;            // [K][64] beta (the NUTS variate v)
   double* vec;             // [K][MMB_LG_NVEC][64]
@@ -36,8 +38,8 @@ struct LgArgs {
   double* draws;           // [n_kept][p][K] or null
   // gradient exchange between the two kernels
   double* pos;             // [K][64] positions of the chains that requested a gradient (slot order)
-  double* gpart;           // [MMB_LG_NR][K][64]
-  double* lpart;           // [MMB_LG_NR][K]
+  double* gpart;           // [MMB_LG_NG][K][64] group partials
+  double* lpart;           // [MMB_LG_NG][K]
   int32_t* count;          // [2] requests in the current step (ping-pong by step parity)
   unsigned long long* ngrad;  // total gradient evaluations of the window
 };

@@ -8,8 +8,8 @@
 //   lp  = y .* eta - softplus(eta),  res = y - invlogit(eta)      (fused, registers)
 //   G   = X' * res                   (64 x N)·(N x slots), f64 MFMA, D regs of the first
 //                                    GEMM reused directly as B operands of the second
-// as MMB_LG_NR row-range partials; the next lg_ctl_kernel sums the partials in range order
-// (no atomics: the summation order is fixed and restated by oracle/oracle.c).
+// as MMB_LG_NG group partials; the next lg_ctl_kernel sums them in group order (no atomics:
+// the summation order is the mmb_math.h spec, restated by oracle/oracle.c).
 #include "logistic.h"
 #include "nuts.h"
 
@@ -69,7 +69,7 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   const double sd2 = A.prior_sd * A.prior_sd;
   double gg = el ? -x / sd2 : 0.0;
 #pragma unroll 4
-  for (int rg = 0; rg < MMB_LG_NR; ++rg) gg = gg + A.gpart[((size_t)rg * A.K + slot) * 64 + lane];
+  for (int rg = 0; rg < MMB_LG_NG; ++rg) gg = gg + A.gpart[((size_t)rg * A.K + slot) * 64 + lane];
   if (!isfinite(gg)) gg = 0.0;
   S.g[0] = el ? gg : 0.0;
   const bool bad = el && !isfinite(x);
@@ -78,7 +78,7 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   double lf = 0.0 + (__ballot(bad) ? -__builtin_inf() : d_iso(A.p, A.prior_sd, ssq));
   if (isfinite(lf)) {
     double ylp = 0.0;
-    for (int rg = 0; rg < MMB_LG_NR; ++rg) ylp = ylp + A.lpart[(size_t)rg * A.K + slot];
+    for (int rg = 0; rg < MMB_LG_NG; ++rg) ylp = ylp + A.lpart[(size_t)rg * A.K + slot];
     lf = lf + ylp;
   }
   S.lf = lf;
@@ -133,17 +133,27 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
   }
 }
 
-// grid (ceil(K/64), MMB_LG_NR), 256 threads: wave w handles slots [64*bx + 16*w, +16) over
-// the rows of range blockIdx.y.  Lane l: chain column l & 15, k-group l >> 4.
+// 1-D grid of 16 * ceil(K/16) workgroups of 4 waves.  Workgroup -> (group gi, chain tile):
+// blocks are dealt round-robin over the 8 XCDs, so XCD x gets groups 2x and 2x+1 only and its
+// L2 holds just those rows of X; tiles ascend with the block id, so the blocks beyond the
+// active count (the end of a window) are the last dispatched and exit at once.
+// Wave w computes sub-range 4*gi + w for the tile's 16 chains; the 4 sub-range partials are
+// combined through LDS in the spec order.  Lane l: chain column l & 15, k-group l >> 4.
 __global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity) {
+  __shared__ double red[MMB_LG_NS][4][4][64];  // [wave][p-tile][reg][lane]
+  __shared__ double lred[MMB_LG_NS][16];
   const int nact = A.count[parity];
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
-  if ((int)blockIdx.x * 64 >= nact) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
+  const int b = (int)blockIdx.x;
+  const int idx = b >> 3;
+  const int gi = 2 * (b & 7) + (idx & 1);
+  const int tile = idx >> 1;
+  if (tile * 16 >= nact) return;
+  const int w = (int)(threadIdx.x >> 6);
   const int l = (int)(threadIdx.x & 63);
   const int lc = l & 15, lq = l >> 4;
-  const int slot = (int)blockIdx.x * 64 + (int)(threadIdx.x >> 6) * 16 + lc;
+  const int slot = tile * 16 + lc;
   const bool live = slot < nact;
-  const int rg = (int)blockIdx.y;
   double bpos[13];
 #pragma unroll
   for (int kk = 0; kk < 13; ++kk) bpos[kk] = live ? A.pos[(size_t)slot * 64 + 4 * kk + lq] : 0.0;
@@ -151,13 +161,15 @@ __global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
   double lsum = 0.0;
-  const int nb = A.rpr / 16;
-  for (int b = 0; b < nb; ++b) {
-    const int r0 = rg * A.rpr + 16 * b;
-    const double* xa = A.X + (size_t)(r0 + lc) * 64 + lq;
+  const int nb = A.rps / 16;
+  const int rbase = (gi * MMB_LG_NS + w) * A.rps;
+  for (int bk = 0; bk < nb; ++bk) {
+    const int r0 = rbase + 16 * bk;
+    const double* xa = A.Xt + (size_t)lq * A.Np + r0 + lc;
     mmb_d4 eta = mmb_d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int kk = 0; kk < 13; ++kk) eta = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[4 * kk], bpos[kk], eta, 0, 0, 0);
+    for (int kk = 0; kk < 13; ++kk)
+      eta = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np], bpos[kk], eta, 0, 0, 0);
     double s[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -176,13 +188,22 @@ __global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity
   }
   lsum = lsum + __shfl_xor(lsum, 16, 64);
   lsum = lsum + __shfl_xor(lsum, 32, 64);
-  if (!live) return;
-  if (lq == 0) A.lpart[(size_t)rg * A.K + slot] = lsum;
-  double* gp = A.gpart + ((size_t)rg * A.K + slot) * 64;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) gp[16 * mt + lq + 4 * q] = acc[mt][q];
+    for (int q = 0; q < 4; ++q) red[w][mt][q][l] = acc[mt][q];
+  if (l < 16) lred[w][l] = lsum;
+  __syncthreads();
+  if (!live) return;
+  // wave w writes p-tile w: coefficient 16w + lq + 4q of chain lc
+  double* gp = A.gpart + ((size_t)gi * A.K + slot) * 64;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double v = ((red[0][w][q][l] + red[1][w][q][l]) + red[2][w][q][l]) + red[3][w][q][l];
+    gp[16 * w + lq + 4 * q] = v;
+  }
+  if (w == 0 && lq == 0)
+    A.lpart[(size_t)gi * A.K + slot] = ((lred[0][lc] + lred[1][lc]) + lred[2][lc]) + lred[3][lc];
 }
 
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st) {
@@ -190,6 +211,6 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t
   return hipGetLastError();
 }
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {
-  hipLaunchKernelGGL(lg_grad_kernel, dim3((A.K + 63) / 64, MMB_LG_NR), dim3(256), 0, st, A, parity);
+  hipLaunchKernelGGL(lg_grad_kernel, dim3(16 * ((A.K + 15) / 16)), dim3(256), 0, st, A, parity);
   return hipGetLastError();
 }

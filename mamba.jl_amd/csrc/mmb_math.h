@@ -296,13 +296,16 @@ MMB_HD double mmb_gamma_mt(double a, const mmb_rng* sn, const mmb_rng* su, uint3
 
 /* ---- logistic likelihood (BASELINE config 4): y ~ Bernoulli(invlogit(eta)).
  * Per observation: log-density y*eta - softplus(eta) and score residual y - invlogit(eta),
- * both from t = exp(-|eta|) (stable for any eta).  The batched gradient sums over rows in
- * MMB_LG_NR fixed row ranges of mmb_lg_rpr(N) rows (a multiple of 16, the MFMA tile);
- * the range structure is part of the summation spec that the oracle restates. */
-#define MMB_LG_NR 16
+ * both from t = exp(-|eta|) (stable for any eta).  Summation spec of the batched gradient
+ * (restated by the oracle): rows are split into MMB_LG_NG groups of MMB_LG_NS sub-ranges of
+ * mmb_lg_rps(N) rows (a multiple of the 16-row MFMA tile).  Within a sub-range each
+ * gradient component is one fma chain over its rows in order; a group's partial is
+ * ((P0 + P1) + P2) + P3; the gradient is -beta/sd^2 + G0 + G1 + ... in group order. */
+#define MMB_LG_NG 16
+#define MMB_LG_NS 4
 #define MMB_LG_DV 64 /* coefficients per chain, padded (p <= 64) */
-MMB_HD int mmb_lg_rpr(int N) {
-  int per = (N + MMB_LG_NR - 1) / MMB_LG_NR;
+MMB_HD int mmb_lg_rps(int N) {
+  int per = (N + MMB_LG_NG * MMB_LG_NS - 1) / (MMB_LG_NG * MMB_LG_NS);
   return ((per + 15) / 16) * 16;
 }
 MMB_HD void mmb_logistic_terms(double eta, double y, double* lp, double* res) {
