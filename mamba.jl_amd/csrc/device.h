@@ -57,6 +57,16 @@ struct SweepArgs {
   const DBlock* blocks;  // device array [nb] (uniform, scalar-cache loads)
 };
 
+// Block descriptors are read-only for a launch: read them through the constant address
+// space so uniform accesses become scalar loads (s_load, scalar cache).
+__device__ __forceinline__ const DBlock& mmb_block(const DBlock* p, int b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const DBlock*)&((const __attribute__((address_space(4))) DBlock*)p)[b];
+#else
+  return p[b];
+#endif
+}
+
 MMB_HD int mmb_tri(int i) { return (i * (i + 1)) >> 1; }
 MMB_HD int mmb_slot(int i, int k) { return i >= k ? mmb_tri(i) + k : mmb_tri(k) + i; }
 

@@ -9,6 +9,7 @@
 template <class M>
 struct Smp {
   static constexpr int G = M::G, R = M::R, DMAX = M::DMAX, DP = M::DP, TP = M::TP;
+  static constexpr int NT = (TP + G - 1) / G;  // packed-triangle slots per lane
   using St = typename M::St;
   using Lc = typename M::Lc;
 
@@ -117,6 +118,12 @@ struct Smp {
         }
         int p;
         double val;
+#ifdef MMB_EXP_NOPIVOT
+        if (G == 32) {  // timing experiment only: no pivot search
+          p = j;
+          val = __shfl(dl[0], (int)(threadIdx.x & 32) + j, 64);
+        } else
+#endif
         if (G == 32) {
           // fast path: max-reduce, then the (usually unique) lane holding it
           double mx = cand[0];
@@ -215,6 +222,7 @@ struct Smp {
             int e = r * G + g.lane;
             if (!done[r]) {
               double t0 = 0.0, t1 = 0.0;
+#ifndef MMB_EXP_NODOT
 #pragma unroll
               for (int k = 0; k + 1 < j; k += 2) {
                 const double2 pp = *(const double2*)(prow + k);
@@ -222,6 +230,7 @@ struct Smp {
                 t1 = fma(Lrow[r][k + 1], pp.y, t1);
               }
               if (j & 1) t0 = fma(Lrow[r][j - 1], prow[j - 1], t0);
+#endif
               double lij = (mat[mmb_slot(e, p)] - (t0 + t1)) * rinv;
               Lrow[r][j] = lij;
               work[r] = work[r] + lij * lij;
@@ -326,7 +335,12 @@ struct Smp {
       if (fl & 4) {
         grp_sync();
         const double* Ls = B.t_Ls + (size_t)c * TP;
-        for (int t = g.lane; t < T; t += G) mat[t] = Ls[t];
+        double lt[NT];  // all loads issued before the first use (one HBM latency, not NT)
+#pragma unroll
+        for (int u = 0; u < NT; ++u) lt[u] = (u * G + g.lane < T) ? Ls[u * G + g.lane] : 0.0;
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+          if (u * G + g.lane < T) mat[u * G + g.lane] = lt[u];
         const uint8_t* pv = B.t_piv + (size_t)c * DP;
         for (int k = g.lane; k < d; k += G) {
           int pk_ = pv[k];
@@ -397,16 +411,28 @@ struct Smp {
         }
         grp_sync();
       }
+      if (!fresh) {  // stage Mvv in LDS: all loads in flight at once (one HBM latency)
+        double lt[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) lt[u] = (u * G + g.lane < T) ? Mvv[u * G + g.lane] : 0.0;
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+          if (u * G + g.lane < T) mat[u * G + g.lane] = lt[u];
+      }
       int si, sk;  // (i, k) of slot g.lane, then stepped by G slots per iteration
       slot_ik(g.lane, si, sk);
-      for (int t = g.lane; t < T; t += G) {
-        const int i = si, k = sk;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int t = u * G + g.lane;
+        if (t < T) {
+          const int i = si, k = sk;
+          double old = fresh ? z2s[i] * z2s[k] : mat[t];
+          double nv = p * old + (q * vvs[k]) * vvs[i];
+          Mvv[t] = nv;
+          mat[t] = cc * (nv - mvs[k] * mvs[i]);
+        }
         sk += G;
         while (sk > si) { sk -= si + 1; ++si; }
-        double old = fresh ? z2s[i] * z2s[k] : Mvv[t];
-        double nv = p * old + (q * vvs[k]) * vvs[i];
-        Mvv[t] = nv;
-        mat[t] = cc * (nv - mvs[k] * mvs[i]);
       }
       grp_sync();
       // everything but the factorization is finished first; the chain state is parked
@@ -422,11 +448,17 @@ struct Smp {
       M::stash(stq, s, g.lane);
       int* pks = (int*)z2s;  // pivot order (group-uniform values), LDS
       grp_sync();
+#ifdef MMB_EXP_NOPCHOL
+      int rank = d;  // timing experiment only
+#else
       int rank = pchol(d, mat, (double*)ia, pks, g);
+#endif
       grp_sync();
       if (rank == d) {
         double* Ls = B.t_Ls + (size_t)c * TP;
-        for (int t = g.lane; t < T; t += G) Ls[t] = mat[t];
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+          if (u * G + g.lane < T) Ls[u * G + g.lane] = mat[u * G + g.lane];
         uint8_t* pv = B.t_piv + (size_t)c * DP;
         for (int k = g.lane; k < d; k += G) pv[k] = (uint8_t)pks[k];
         if (g.lane == 0) B.t_flags[c] = fl | 4;

@@ -32,7 +32,9 @@ __global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const Sweep
   for (int step = 0; step < A.n_iters; ++step) {
     const int64_t it = A.iter0 + 1 + step;
     for (int b = 0; b < A.nb; ++b) {
-      const DBlock& B = A.blocks[b];  // global memory, uniform index
+      // descriptor read through the constant address space: uniform scalar loads (s_load,
+      // scalar cache) instead of vector loads that wait on the vector memory path
+      const DBlock& B = mmb_block(A.blocks, b);
       const mmb_rng rn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_NORMAL);
       const mmb_rng ru = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_UNIFORM);
       const bool adapt = B.adapt == MMB_ADAPT_ALL ? true
