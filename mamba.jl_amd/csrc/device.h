@@ -190,6 +190,27 @@ struct Grp {
   }
 };
 
+// Phase timing (profiling builds only, -DMMB_PHASE_PROF): per-phase s_memtime cycles summed
+// over lane groups into mmb_prof[]; engine.cpp prints them at mmb_destroy.
+#ifdef MMB_PHASE_PROF
+extern __device__ unsigned long long mmb_prof[32];
+// per-wave accumulators in LDS (lane 0 of each wave), flushed once per kernel
+__device__ __forceinline__ unsigned long long* mmb_prof_lds() {
+  __shared__ unsigned long long p[4][16];
+  return p[threadIdx.x >> 6];
+}
+#define MMB_PROF_START uint64_t _mmb_t0 = __builtin_amdgcn_s_memtime();
+#define MMB_PROF_MARK(i, lane)                                              \
+  {                                                                         \
+    uint64_t _mmb_t1 = __builtin_amdgcn_s_memtime();                        \
+    if ((threadIdx.x & 63) == 0) mmb_prof_lds()[(i)] += _mmb_t1 - _mmb_t0;  \
+    _mmb_t0 = _mmb_t1;                                                      \
+  }
+#else
+#define MMB_PROF_START
+#define MMB_PROF_MARK(i, lane)
+#endif
+
 // Julia min(a, b): NaN propagates
 __device__ __forceinline__ double jmin(double a, double b) {
   if (isnan(a)) return a;

@@ -310,10 +310,17 @@ static void free_dev(mmb_engine* e) {
   e->draws_cap = 0;
 }
 
+#ifdef MMB_PHASE_PROF
+void mmb_prof_dump();
+#endif
+
 void mmb_destroy(mmb_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+#ifdef MMB_PHASE_PROF
+  mmb_prof_dump();
+#endif
   free_dev(e);
   if (e->d_data) (void)hipFree(e->d_data);
   if (e->lg_X) (void)hipFree(e->lg_X);

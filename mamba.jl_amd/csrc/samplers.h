@@ -264,9 +264,11 @@ struct Smp {
     return rank;
   }
 
+  // (i, k) of packed slot s = tri(i) + k: float square root estimate, integer correction
   __device__ __forceinline__ static void slot_ik(int s, int& i, int& k) {
-    int ii = 0;
-    while (mmb_tri(ii + 1) <= s) ++ii;
+    int ii = (int)((sqrtf((float)(8 * s + 1)) - 1.0f) * 0.5f);
+    ii += (mmb_tri(ii + 1) <= s) ? 1 : 0;
+    ii -= (mmb_tri(ii) > s) ? 1 : 0;
     i = ii;
     k = s - mmb_tri(ii);
   }
@@ -284,6 +286,7 @@ struct Smp {
     double* mvs = vvs + DP;
     int* ia = (int*)(mvs + DP);  // piv / pos scratch (2*DP ints)
     double v[R], x[R], z1[R], z2[R], mv[R];
+    MMB_PROF_START
     M::unlist(B, s, g.lane, v);
     int m = B.t_m[c];
     int fl = B.t_flags[c];
@@ -300,6 +303,7 @@ struct Smp {
       for (int r = 0; r < R; ++r) mv[r] = v[r];
     }
     fl = adapt ? (fl | 1) : (fl & ~1);
+    MMB_PROF_MARK(1, g.lane)
     // proposal: x = SigmaL * z1 [; x = beta*x + (1-beta)*SigmaLm*z2]; x += v
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -341,12 +345,12 @@ struct Smp {
 #pragma unroll
         for (int u = 0; u < NT; ++u)
           if (u * G + g.lane < T) mat[u * G + g.lane] = lt[u];
-        const uint8_t* pv = B.t_piv + (size_t)c * DP;
-        for (int k = g.lane; k < d; k += G) {
-          int pk_ = pv[k];
-          ia[k] = pk_;
-          ia[DP + pk_] = k;
-        }
+        // pivot order: the chain's DP bytes as DP/4 words in registers (uniform per group),
+        // so the matvec's LDS reads are independent of each other (no ia[k] -> mat chain)
+        uint32_t pw[DP / 4];
+        const uint32_t* pvw = (const uint32_t*)(B.t_piv + (size_t)c * DP);
+#pragma unroll
+        for (int w = 0; w < DP / 4; ++w) pw[w] = pvw[w];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           int e = r * G + g.lane;
@@ -355,14 +359,22 @@ struct Smp {
         grp_sync();
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          int e = r * G + g.lane;
-          if (e < d) {
-            int pe = ia[DP + e];
-            double a = 0.0;
-            for (int k = 0; k < pe; ++k) a = fma(mat[mmb_slot(e, ia[k])], z2s[k], a);
-            a = fma(mat[mmb_tri(e) + e], z2s[pe], a);
-            y[r] = a;
+          const int e = r * G + g.lane;
+          int pe = 0;  // position of e in the pivot order
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k)
+            if (k < d && (int)((pw[k >> 2] >> (8 * (k & 3))) & 0xffu) == e) pe = k;
+          double a = 0.0;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) {
+            if (k < d) {
+              const int q = (int)((pw[k >> 2] >> (8 * (k & 3))) & 0xffu);
+              const double m_ = mat[mmb_slot(e, q)];
+              const double z_ = z2s[k];
+              a = (k < pe) ? fma(m_, z_, a) : a;
+            }
           }
+          if (e < d) y[r] = fma(mat[mmb_tri(e) + e], z2s[pe], a);
         }
       }
 #pragma unroll
@@ -370,6 +382,7 @@ struct Smp {
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = x[r] + v[r];
+    MMB_PROF_MARK(2, g.lane)
     const typename M::Prep pc = M::prep(B, s);
     double lx = M::logf_p(A, B, pc, s, l, g, x);
     double lv = M::logf_p(A, B, pc, s, l, g, v);
@@ -377,6 +390,7 @@ struct Smp {
 #pragma unroll
       for (int r = 0; r < R; ++r) v[r] = x[r];
     }
+    MMB_PROF_MARK(3, g.lane)
     if (adapt) {  // amm.jl:196-206
       m += 1;
       const double p = (double)m / ((double)m + 1.0);
@@ -419,20 +433,17 @@ struct Smp {
         for (int u = 0; u < NT; ++u)
           if (u * G + g.lane < T) mat[u * G + g.lane] = lt[u];
       }
-      int si, sk;  // (i, k) of slot g.lane, then stepped by G slots per iteration
-      slot_ik(g.lane, si, sk);
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         const int t = u * G + g.lane;
         if (t < T) {
-          const int i = si, k = sk;
+          int i, k;
+          slot_ik(t, i, k);
           double old = fresh ? z2s[i] * z2s[k] : mat[t];
           double nv = p * old + (q * vvs[k]) * vvs[i];
           Mvv[t] = nv;
           mat[t] = cc * (nv - mvs[k] * mvs[i]);
         }
-        sk += G;
-        while (sk > si) { sk -= si + 1; ++si; }
       }
       grp_sync();
       // everything but the factorization is finished first; the chain state is parked
@@ -448,12 +459,14 @@ struct Smp {
       M::stash(stq, s, g.lane);
       int* pks = (int*)z2s;  // pivot order (group-uniform values), LDS
       grp_sync();
+      MMB_PROF_MARK(4, g.lane)
 #ifdef MMB_EXP_NOPCHOL
       int rank = d;  // timing experiment only
 #else
       int rank = pchol(d, mat, (double*)ia, pks, g);
 #endif
       grp_sync();
+      MMB_PROF_MARK(5, g.lane)
       if (rank == d) {
         double* Ls = B.t_Ls + (size_t)c * TP;
 #pragma unroll
@@ -465,6 +478,7 @@ struct Smp {
       }
       M::unstash(stq, s, g.lane);
       grp_sync();
+      MMB_PROF_MARK(6, g.lane)
       return;
     }
 #pragma unroll

@@ -9,6 +9,18 @@
 // pivoted Cholesky factor are staged in LDS.
 #include "samplers.h"
 
+#ifdef MMB_PHASE_PROF
+#include <cstdio>
+__device__ unsigned long long mmb_prof[32];
+void mmb_prof_dump() {
+  unsigned long long h[32];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mmb_prof), sizeof h) != hipSuccess) return;
+  const char* names[] = {"-", "amm:load m/fl/Mv", "amm:proposal", "amm:logf x2+accept", "amm:moments+Sigma",
+                         "amm:pchol", "amm:store", "gibbs", "iteration", "count"};
+  for (int i = 1; i < 10; ++i) fprintf(stderr, "MMB_PROF %-22s %llu\n", names[i], h[i]);
+}
+#endif
+
 #ifndef MMB_SWEEP_WAVES
 #define MMB_SWEEP_WAVES 3  // min waves per SIMD the register allocator must allow
 #endif
@@ -29,8 +41,15 @@ __global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const Sweep
   typename M::Lc l;
   M::load(A, c, g.lane, s, l);
   const uint32_t chain = A.chain_offset + (uint32_t)c;
+#ifdef MMB_PHASE_PROF
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < 16; ++i) mmb_prof_lds()[i] = 0;
+#endif
   for (int step = 0; step < A.n_iters; ++step) {
     const int64_t it = A.iter0 + 1 + step;
+#ifdef MMB_PHASE_PROF
+    const uint64_t _it0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int b = 0; b < A.nb; ++b) {
       // descriptor read through the constant address space: uniform scalar loads (s_load,
       // scalar cache) instead of vector loads that wait on the vector memory path
@@ -58,13 +77,21 @@ __global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const Sweep
         case MMB_SAMPLER_GIBBS: if constexpr ((KINDS >> MMB_SAMPLER_GIBBS) & 1u) {
           const mmb_rng gn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_N);
           const mmb_rng gu = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_U);
+          MMB_PROF_START
           M::gibbs(A, B, s, l, g, &rn, &gn, &gu);
+          MMB_PROF_MARK(7, g.lane)
         }
           break;
         default:
           break;
       }
     }
+#ifdef MMB_PHASE_PROF
+    if ((threadIdx.x & 63) == 0) {
+      mmb_prof_lds()[8] += __builtin_amdgcn_s_memtime() - _it0;
+      mmb_prof_lds()[9] += 1;
+    }
+#endif
     if (A.draws && it > A.burnin && (it - A.burnin) % A.thin == 0 && g.lane == 0) {
       const int64_t row = (it - A.burnin) / A.thin - 1 - A.kept_origin;
       double mon[M::PMON];
@@ -74,6 +101,10 @@ __global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const Sweep
     }
   }
   M::store(A, c, g.lane, s);
+#ifdef MMB_PHASE_PROF
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < 16; ++i) atomicAdd(&mmb_prof[i], mmb_prof_lds()[i]);
+#endif
 }
 
 constexpr unsigned K_ALL = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_AMM) |
