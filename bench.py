@@ -125,9 +125,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch  # noqa: F401  (pins the HIP runtime; RCCL via torch.distributed)
     import torch.distributed as dist
+    # backend "nccl" is RCCL over xGMI; MMB_DIST_BACKEND=gloo rehearses the multi-rank path
+    # on a single GPU (ranks share the device, the all-reduces run on host tensors)
+    backend = os.environ.get("MMB_DIST_BACKEND", "nccl")
+    local = local % max(torch.cuda.device_count(), 1)
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
     import _mamba_path
     mb = _mamba_path.load()
     import numpy as np
@@ -155,7 +163,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     total_units = K * world * args.steps
@@ -163,24 +171,23 @@ def main():
     grads_timed = eng.grad_evals() if nuts else 0
 
     psrf = None
-    if eng.pmon <= 4:
-        # Gelman-Rubin over all chains of all GPUs: device partials + one RCCL all-reduce
-        def ar_sum(x):
-            if world == 1:
-                return x
-            t = torch.tensor(x, dtype=torch.float64, device="cuda")
-            dist.all_reduce(t)
-            return t.cpu().numpy()
+    # Gelman-Rubin over all chains of all GPUs: device partials + one RCCL all-reduce
+    def ar_sum(x):
+        if world == 1:
+            return x
+        t = torch.tensor(x, dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t)
+        return t.cpu().numpy()
 
-        def ar_minmax(lo, hi):
-            if world == 1:
-                return lo, hi
-            a = torch.tensor(np.concatenate([-lo, hi]), dtype=torch.float64, device="cuda")
-            dist.all_reduce(a, op=dist.ReduceOp.MAX)
-            a = a.cpu().numpy()
-            return -a[:len(lo)], a[len(lo):]
+    def ar_minmax(lo, hi):
+        if world == 1:
+            return lo, hi
+        a = torch.tensor(np.concatenate([-lo, hi]), dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(a, op=dist.ReduceOp.MAX)
+        a = a.cpu().numpy()
+        return -a[:len(lo)], a[len(lo):]
 
-        psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax)
+    psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax)
 
     # roofline of the dominant kernel; per-launch device time from HIP events on the engine's stream
     if nuts:  # lg_grad_kernel: 4*N*p algorithmic flops per gradient (X*beta and X'*res)
@@ -232,7 +239,7 @@ def main():
                  "line.jl data; synthetic inits" if args.workload == "line_amm" else
                  "synthetic X ~ N(0,1), y ~ Bernoulli(invlogit(X beta_true)) (SURVEY §8d seeds); inits N(0, 0.1^2)"),
         "config": {"workload": desc, "chains_per_gpu": K, "global_chains": K * world, "thin": thin,
-                   "parallelism": f"chain-shard x{world}"},
+                   "parallelism": f"chain-shard x{world}", "collective": "rccl" if backend == "nccl" else backend},
         "roofline": roof,
     }
     if args.workload != "rats":

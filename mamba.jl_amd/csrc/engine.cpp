@@ -915,7 +915,6 @@ int64_t mmb_gr_len(const mmb_engine* e) {
 
 int mmb_gr_range(mmb_engine* e, double* minmax) {
   if (!e || !minmax) return fail(e, MMB_E_ARG, "null argument");
-  if (e->pmon > 4) return fail(e, MMB_E_UNSUPPORTED, "device Gelman-Rubin supports <= 4 monitored values");
   if (e->n_kept < 1) return fail(e, MMB_E_STATE, "no device-kept draws (run with keep_device=1)");
   HIPCHK(e, hipSetDevice(e->device));
   double* d = nullptr;
@@ -930,7 +929,6 @@ int mmb_gr_range(mmb_engine* e, double* minmax) {
 
 int mmb_gr_partials(mmb_engine* e, const int32_t* link, const double* shift, double* out) {
   if (!e || !link || !shift || !out) return fail(e, MMB_E_ARG, "null argument");
-  if (e->pmon > 4) return fail(e, MMB_E_UNSUPPORTED, "device Gelman-Rubin supports <= 4 monitored values");
   if (e->n_kept < 2) return fail(e, MMB_E_STATE, "need >= 2 device-kept draws per chain");
   HIPCHK(e, hipSetDevice(e->device));
   const int p = e->pmon;

@@ -124,11 +124,15 @@ static hipError_t launch(const SweepArgs& A, hipStream_t st, int threads) {
 }
 
 // host-side launcher (engine.cpp); kinds = bitmask of the scheme's sampler kinds
+#ifndef MMB_RATS_BLOCK
+#define MMB_RATS_BLOCK 256
+#endif
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st) {
   if (model == MMB_MODEL_RATS) {
-    if ((kinds & ~K_GIBBS_AMM) == 0) return launch<MMB_MODEL_RATS, K_GIBBS_AMM>(A, st, 256);
-    if ((kinds & ~K_SLICE_AMWG) == 0) return launch<MMB_MODEL_RATS, K_SLICE_AMWG>(A, st, 256);
-    return launch<MMB_MODEL_RATS, K_ALL>(A, st, 256);
+    constexpr int TB = MMB_RATS_BLOCK;
+    if ((kinds & ~K_GIBBS_AMM) == 0) return launch<MMB_MODEL_RATS, K_GIBBS_AMM>(A, st, TB);
+    if ((kinds & ~K_SLICE_AMWG) == 0) return launch<MMB_MODEL_RATS, K_SLICE_AMWG>(A, st, TB);
+    return launch<MMB_MODEL_RATS, K_ALL>(A, st, TB);
   }
   if (model == MMB_MODEL_LINE) {
     if (kinds & (1u << MMB_SAMPLER_NUTS)) return launch<MMB_MODEL_LINE, K_ALL_NUTS>(A, st, 64);

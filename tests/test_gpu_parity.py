@@ -146,3 +146,16 @@ def test_logistic_nuts_parity(mamba, oracle):
     np.testing.assert_array_equal(dg, do)
     np.testing.assert_array_equal(eng.values(), st["values"])
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+
+
+def test_logistic_device_gelman_rubin_matches_host(mamba):
+    """p = 50 monitored values: the workgroup-per-chain-chunk Gelman-Rubin kernel."""
+    m, _ = logistic(mamba, 1000, 50)
+    eng = mamba.Engine(m)
+    eng.init_chains(np.random.default_rng(3).normal(0.0, 0.1, (40, 50)), seed=4)
+    d = eng.run(60, burnin=20, thin=1, model_burnin=20, keep_device=True)
+    for transform in (False, True):
+        ps_dev, mp_dev = mamba.gelmandiag_sharded(eng, transform=transform, mpsrf=True)
+        ps_host, mp_host = mamba.gelmandiag(d, transform=transform, mpsrf=True)
+        np.testing.assert_allclose(ps_dev, ps_host, rtol=1e-8)
+        assert mp_dev == pytest.approx(mp_host, rel=1e-6)
