@@ -18,7 +18,7 @@ struct Mdl;
 template <>
 struct Mdl<MMB_MODEL_RATS> {
   static constexpr int G = 32, R = 1, DMAX = 30, DP = 32, TP = 480, VS = 72, PMON = 3;
-  static constexpr int LDS_DBL = TP + 4 * DP + 2 * DP + 8;  // matrix, 4 vectors, state stash
+  static constexpr int LDS_DBL = TP + 4 * DP;  // matrix + 4 vectors (the stash reuses idle ones)
   struct St { double a, b, s2c, mua, s2a, mub, s2b; };
   struct Lc { const double* y; };  // this lane's 5 observations (global, L1-resident)
 
@@ -44,21 +44,20 @@ struct Mdl<MMB_MODEL_RATS> {
   __device__ __forceinline__ static bool positive(int node) {
     return node == MMB_RATS_S2_C || node == MMB_RATS_S2_ALPHA || node == MMB_RATS_S2_BETA;
   }
-  // park the chain state in LDS across a register-heavy phase (pivoted Cholesky)
-  static constexpr int STASH_DBL = 2 * DP + 8;
-  __device__ __forceinline__ static void stash(double* q, const St& s, int lane) {
-    q[lane] = s.a;
-    q[DP + lane] = s.b;
-    if (lane == 0) {
-      q[2 * DP + 0] = s.s2c; q[2 * DP + 1] = s.mua; q[2 * DP + 2] = s.s2a;
-      q[2 * DP + 3] = s.mub; q[2 * DP + 4] = s.s2b;
-    }
+  // park the chain state in LDS across a register-heavy phase (pivoted Cholesky), in the
+  // AMM scratch that is idle during it (samplers.h amm(): lds = mat[TP] | z2s | vvs | mvs |
+  // ia): alpha -> vvs, beta -> mvs, scalars -> the tail of z2s (pivot indices use 30 ints)
+  __device__ __forceinline__ static void stash(double* lds, const St& s, int lane) {
+    double* q = lds + TP;
+    q[DP + lane] = s.a;
+    q[2 * DP + lane] = s.b;
+    if (lane == 0) { q[16] = s.s2c; q[17] = s.mua; q[18] = s.s2a; q[19] = s.mub; q[20] = s.s2b; }
   }
-  __device__ __forceinline__ static void unstash(const double* q, St& s, int lane) {
-    s.a = q[lane];
-    s.b = q[DP + lane];
-    s.s2c = q[2 * DP + 0]; s.mua = q[2 * DP + 1]; s.s2a = q[2 * DP + 2];
-    s.mub = q[2 * DP + 3]; s.s2b = q[2 * DP + 4];
+  __device__ __forceinline__ static void unstash(const double* lds, St& s, int lane) {
+    const double* q = lds + TP;
+    s.a = q[DP + lane];
+    s.b = q[2 * DP + lane];
+    s.s2c = q[16]; s.mua = q[17]; s.s2a = q[18]; s.mub = q[19]; s.s2b = q[20];
   }
   // select chains (a switch here is turned into a dynamically indexed private array)
   __device__ __forceinline__ static double scalar(const St& s, int node) {
@@ -235,11 +234,12 @@ struct Mdl<MMB_MODEL_LINE> {
   static constexpr int LDS_DBL = TP + 4 * DP + 8;
   struct St { double v[3]; };
   struct Lc { int dummy; };
-  static constexpr int STASH_DBL = 8;
-  __device__ __forceinline__ static void stash(double* q, const St& s, int) {
+  __device__ __forceinline__ static void stash(double* lds, const St& s, int) {
+    double* q = lds + TP + 4 * DP;
     q[0] = s.v[0]; q[1] = s.v[1]; q[2] = s.v[2];
   }
-  __device__ __forceinline__ static void unstash(const double* q, St& s, int) {
+  __device__ __forceinline__ static void unstash(const double* lds, St& s, int) {
+    const double* q = lds + TP + 4 * DP;
     s.v[0] = q[0]; s.v[1] = q[1]; s.v[2] = q[2];
   }
 

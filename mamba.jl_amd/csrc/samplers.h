@@ -455,8 +455,7 @@ struct Smp {
       }
       if (g.lane == 0) { B.t_m[c] = m; B.t_flags[c] = fl; }
       M::relist(B, s, g, v);
-      double* stq = lds + TP + 4 * DP;
-      M::stash(stq, s, g.lane);
+      M::stash(lds, s, g.lane);
       int* pks = (int*)z2s;  // pivot order (group-uniform values), LDS
       grp_sync();
       MMB_PROF_MARK(4, g.lane)
@@ -476,7 +475,7 @@ struct Smp {
         for (int k = g.lane; k < d; k += G) pv[k] = (uint8_t)pks[k];
         if (g.lane == 0) B.t_flags[c] = fl | 4;
       }
-      M::unstash(stq, s, g.lane);
+      M::unstash(lds, s, g.lane);
       grp_sync();
       MMB_PROF_MARK(6, g.lane)
       return;

@@ -22,7 +22,7 @@ void mmb_prof_dump() {
 #endif
 
 #ifndef MMB_SWEEP_WAVES
-#define MMB_SWEEP_WAVES 3  // min waves per SIMD the register allocator must allow
+#define MMB_SWEEP_WAVES 4  // min waves per SIMD the register allocator must allow
 #endif
 
 // KINDS: bitmask (1 << mmb_sampler_kind) of the sampler kinds present in the scheme; the
