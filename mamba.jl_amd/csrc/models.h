@@ -60,20 +60,26 @@ struct Mdl<MMB_MODEL_RATS> {
     s.s2c = q[16]; s.mua = q[17]; s.s2a = q[18]; s.mub = q[19]; s.s2b = q[20];
   }
   // select chains (a switch here is turned into a dynamically indexed private array)
+  // c ? a : b as an integer bit blend: the optimiser folds a select chain over struct
+  // fields into a load at a computed offset, which forces the chain state to scratch
+  __device__ __forceinline__ static double blend(bool c, double a, double b) {
+    const uint64_t m = 0ull - (uint64_t)c;
+    return mmb_u2d((mmb_d2u(a) & m) | (mmb_d2u(b) & ~m));
+  }
   __device__ __forceinline__ static double scalar(const St& s, int node) {
     double v = s.s2b;
-    v = node == MMB_RATS_S2_C ? s.s2c : v;
-    v = node == MMB_RATS_MU_ALPHA ? s.mua : v;
-    v = node == MMB_RATS_S2_ALPHA ? s.s2a : v;
-    v = node == MMB_RATS_MU_BETA ? s.mub : v;
+    v = blend(node == MMB_RATS_S2_C, s.s2c, v);
+    v = blend(node == MMB_RATS_MU_ALPHA, s.mua, v);
+    v = blend(node == MMB_RATS_S2_ALPHA, s.s2a, v);
+    v = blend(node == MMB_RATS_MU_BETA, s.mub, v);
     return v;
   }
   __device__ __forceinline__ static void set_scalar(St& s, int node, double v) {
-    s.s2c = node == MMB_RATS_S2_C ? v : s.s2c;
-    s.mua = node == MMB_RATS_MU_ALPHA ? v : s.mua;
-    s.s2a = node == MMB_RATS_S2_ALPHA ? v : s.s2a;
-    s.mub = node == MMB_RATS_MU_BETA ? v : s.mub;
-    s.s2b = node == MMB_RATS_S2_BETA ? v : s.s2b;
+    s.s2c = blend(node == MMB_RATS_S2_C, v, s.s2c);
+    s.mua = blend(node == MMB_RATS_MU_ALPHA, v, s.mua);
+    s.s2a = blend(node == MMB_RATS_S2_ALPHA, v, s.s2a);
+    s.mub = blend(node == MMB_RATS_MU_BETA, v, s.mub);
+    s.s2b = blend(node == MMB_RATS_S2_BETA, v, s.s2b);
   }
   __device__ __forceinline__ static int lane_node(const DBlock& B, int lane) {
     int n = B.nodes[0];
@@ -207,21 +213,23 @@ struct Mdl<MMB_MODEL_RATS> {
       double a = 150.0 / 2.0 + 0.001, b = ss / 2.0 + 0.001;
       s.s2c = b / mmb_gamma_mt(a, gn, gu, &kn, &ku);
     } else if (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_MU_BETA) {
-      bool al = n == MMB_RATS_MU_ALPHA;
-      double sum = g.sum(g.lane < 30 ? (al ? s.a : s.b) : 0.0);
-      double s2 = al ? s.s2a : s.s2b;
+      const bool al = n == MMB_RATS_MU_ALPHA;
+      double sum = g.sum(g.lane < 30 ? blend(al, s.a, s.b) : 0.0);
+      double s2 = blend(al, s.s2a, s.s2b);
       double var0 = 1000.0 * 1000.0;
       double vv = 1.0 / (30.0 / s2 + 1.0 / var0);
       double mean = vv * (sum / s2 + 0.0 / var0);
       double v = mean + sqrt(vv) * mmb_normal(rn, 0u);
-      if (al) s.mua = v; else s.mub = v;
+      s.mua = blend(al, v, s.mua);
+      s.mub = blend(al, s.mub, v);
     } else {
-      bool al = n == MMB_RATS_S2_ALPHA;
-      double mu = al ? s.mua : s.mub;
-      double r = (al ? s.a : s.b) - mu;
+      const bool al = n == MMB_RATS_S2_ALPHA;
+      double mu = blend(al, s.mua, s.mub);
+      double r = blend(al, s.a, s.b) - mu;
       double ss = g.sum(g.lane < 30 ? r * r : 0.0);
       double v = (ss / 2.0 + 0.001) / mmb_gamma_mt(30.0 / 2.0 + 0.001, gn, gu, &kn, &ku);
-      if (al) s.s2a = v; else s.s2b = v;
+      s.s2a = blend(al, v, s.s2a);
+      s.s2b = blend(al, s.s2b, v);
     }
   }
 };

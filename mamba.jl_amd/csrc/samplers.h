@@ -435,7 +435,10 @@ struct Smp {
       }
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
-        const int t = u * G + g.lane;
+        int t = u * G + g.lane;
+        // opaque to the optimiser: recomputing (i, k) here is a few VALU ops, while
+        // hoisting all NT pairs out of the iteration loop keeps 2*NT ints live (spills)
+        asm volatile("" : "+v"(t));
         if (t < T) {
           int i, k;
           slot_ik(t, i, k);
