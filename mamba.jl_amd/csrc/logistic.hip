@@ -139,7 +139,10 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
 // active count (the end of a window) are the last dispatched and exit at once.
 // Wave w computes sub-range 4*gi + w for the tile's 16 chains; the 4 sub-range partials are
 // combined through LDS in the spec order.  Lane l: chain column l & 15, k-group l >> 4.
-__global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity) {
+#ifndef MMB_LG_WAVES
+#define MMB_LG_WAVES 3
+#endif
+__global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs A, int parity) {
   __shared__ double red[MMB_LG_NS][4][4][64];  // [wave][p-tile][reg][lane]
   __shared__ double lred[MMB_LG_NS][16];
   const int nact = A.count[parity];
@@ -163,27 +166,44 @@ __global__ __launch_bounds__(256) void lg_grad_kernel(const LgArgs A, int parity
   double lsum = 0.0;
   const int nb = A.rps / 16;
   const int rbase = (gi * MMB_LG_NS + w) * A.rps;
-  for (int bk = 0; bk < nb; ++bk) {
+  // two 16-row blocks per pass: their X*B chains (13 dependent MFMAs each) interleave;
+  // the residual and X'*res steps then run block by block, so every sum keeps row order
+  for (int bk = 0; bk < nb; bk += 2) {
+    const bool two = bk + 1 < nb;
     const int r0 = rbase + 16 * bk;
     const double* xa = A.Xt + (size_t)lq * A.Np + r0 + lc;
-    mmb_d4 eta = mmb_d4{0.0, 0.0, 0.0, 0.0};
+    mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
+    if (two) {
 #pragma unroll
-    for (int kk = 0; kk < 13; ++kk)
-      eta = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np], bpos[kk], eta, 0, 0, 0);
-    double s[4];
+      for (int kk = 0; kk < 13; ++kk) {
+        eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np], bpos[kk], eta0, 0, 0, 0);
+        eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np + 16], bpos[kk], eta1, 0, 0, 0);
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = r0 + lq + 4 * i;
-      double lp = 0.0, res = 0.0;
-      if (row < A.N) mmb_logistic_terms(eta[i], A.y[row], &lp, &res);
-      lsum = lsum + lp;
-      s[i] = res;
+      for (int kk = 0; kk < 13; ++kk)
+        eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np], bpos[kk], eta0, 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double* xt = A.X + (size_t)(r0 + 4 * i + lq) * 64 + lc;
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rb = r0 + 16 * h;
+      const mmb_d4 eta = h ? eta1 : eta0;
+      double s[4];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xt[16 * mt], s[i], acc[mt], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const int row = rb + lq + 4 * i;
+        double lp = 0.0, res = 0.0;
+        if (row < A.N) mmb_logistic_terms(eta[i], A.y[row], &lp, &res);
+        lsum = lsum + lp;
+        s[i] = res;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double* xt = A.X + (size_t)(rb + 4 * i + lq) * 64 + lc;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xt[16 * mt], s[i], acc[mt], 0, 0, 0);
+      }
     }
   }
   lsum = lsum + __shfl_xor(lsum, 16, 64);
