@@ -80,7 +80,9 @@ __device__ __forceinline__ void grp_sync() {
 // ---- cross-lane primitives for 32-lane groups: DPP / permlane (no LDS round trip) ----
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+  // quad_perm / row_mirror / row_half_mirror read a valid lane for every lane, so no
+  // "old" operand is needed (bound_ctrl): no extra v_mov per DPP move
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {

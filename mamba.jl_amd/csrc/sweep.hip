@@ -22,13 +22,18 @@ void mmb_prof_dump() {
 #endif
 
 #ifndef MMB_SWEEP_WAVES
-#define MMB_SWEEP_WAVES 4  // min waves per SIMD the register allocator must allow
+#define MMB_SWEEP_WAVES 4  // rats: min waves per SIMD the register allocator must allow
 #endif
+// Occupancy target per model: rats runs 8192 waves and is latency-bound (4 waves/SIMD
+// measured 12 % faster than 3 despite spills); line has 64 waves in all, so it keeps the
+// whole register budget (no spills).
+template <int MODEL>
+constexpr int sweep_waves() { return MODEL == MMB_MODEL_RATS ? MMB_SWEEP_WAVES : 1; }
 
 // KINDS: bitmask (1 << mmb_sampler_kind) of the sampler kinds present in the scheme; the
 // other block paths are compiled out (register/SGPR allocation is per kernel).
 template <int MODEL, unsigned KINDS>
-__global__ __launch_bounds__(256, MMB_SWEEP_WAVES) void sweep_kernel(const SweepArgs A) {
+__global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const SweepArgs A) {
   using M = Mdl<MODEL>;
   using S = Smp<M>;
   constexpr int G = M::G;
