@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 1
+#define MMB_ABI_VERSION 2
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -57,14 +57,16 @@ enum {
 };
 enum { MMB_LOGISTIC_BETA = 0 };
 
-/* ---- sampler kinds (src/samplers/{amwg,amm,nuts,slice}.jl) ---- */
+/* ---- sampler kinds (src/samplers/{amwg,amm,nuts,slice,hmc,mala}.jl) ---- */
 typedef enum {
   MMB_SAMPLER_AMWG = 1,  /* src/samplers/amwg.jl:47-61 */
   MMB_SAMPLER_AMM = 2,   /* src/samplers/amm.jl:45-59    */
   MMB_SAMPLER_NUTS = 3,  /* src/samplers/nuts.jl:47-56 */
   MMB_SAMPLER_SLICE = 4, /* src/samplers/slice.jl:47-58 */
-  MMB_SAMPLER_GIBBS = 5  /* user Sampler(params, f): conjugate full conditional of the block's node,
+  MMB_SAMPLER_GIBBS = 5, /* user Sampler(params, f): conjugate full conditional of the block's node,
                             e.g. doc/tutorial/line.jl:168-186 */
+  MMB_SAMPLER_HMC = 6,   /* src/samplers/hmc.jl:47-65 */
+  MMB_SAMPLER_MALA = 7   /* src/samplers/mala.jl:43-58 */
 } mmb_sampler_kind;
 
 typedef enum { MMB_ADAPT_ALL = 0, MMB_ADAPT_BURNIN = 1, MMB_ADAPT_NONE = 2 } mmb_adapt;
@@ -84,7 +86,11 @@ typedef struct {
   double scale;                            /* AMM scale (2.38) */
   int32_t dim;                             /* unlisted block length (checked by mmb_create) */
   int32_t ntuning;                         /* length of `tuning` */
-  const double* tuning;                    /* AMWG sigma[dim] | Slice width[dim] | AMM Sigma[dim*dim] col-major */
+  const double* tuning;                    /* AMWG sigma[dim] | Slice width[dim] | AMM Sigma[dim*dim] col-major
+                                              | HMC/MALA Sigma[dim*dim] col-major, or none (SigmaL = I) */
+  double epsilon;                          /* HMC/MALA step size (hmc.jl:13, mala.jl:12) */
+  int32_t nsteps;                          /* HMC leapfrog steps L (hmc.jl:13) */
+  int32_t reserved;
 } mmb_block_spec;
 
 typedef struct {

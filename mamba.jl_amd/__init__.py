@@ -11,7 +11,7 @@ from . import abi, gelman, model, samplers  # noqa: F401
 from .gelman import gelmandiag, gelmandiag_sharded, psrf_from_sums  # noqa: F401
 from .mcmc import Chains, Engine, mcmc, mcmc_restart  # noqa: F401
 from .model import line, logistic, rats  # noqa: F401
-from .samplers import (AMM, AMWG, NUTS, ArgumentError, Gibbs, Multivariate, Sampler,  # noqa: F401
+from .samplers import (AMM, AMWG, HMC, MALA, NUTS, ArgumentError, Gibbs, Multivariate, Sampler,  # noqa: F401
                        Slice, Univariate)
 
 __version__ = "0.1.0"

@@ -12,6 +12,8 @@ MMB_MAX_NODES_PER_BLOCK = 4
 
 MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = 1, 2, 3
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
+MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
+MMB_ABI_VERSION = 2
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
 MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
 MMB_LINE_BETA, MMB_LINE_S2 = 0, 1
@@ -28,7 +30,8 @@ class BlockSpec(C.Structure):
                 ("nodes", C.c_int32 * MMB_MAX_NODES_PER_BLOCK), ("adapt", C.c_int32),
                 ("form", C.c_int32), ("transform", C.c_int32), ("batchsize", C.c_int32),
                 ("target", C.c_double), ("beta", C.c_double), ("scale", C.c_double),
-                ("dim", C.c_int32), ("ntuning", C.c_int32), ("tuning", C.POINTER(C.c_double))]
+                ("dim", C.c_int32), ("ntuning", C.c_int32), ("tuning", C.POINTER(C.c_double)),
+                ("epsilon", C.c_double), ("nsteps", C.c_int32), ("reserved", C.c_int32)]
 
 
 class ModelSpec(C.Structure):
@@ -94,7 +97,7 @@ def lib():
         except Exception:
             pass
         _lib = _declare(C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL))
-        if _lib.mmb_abi_version() != 1:
+        if _lib.mmb_abi_version() != MMB_ABI_VERSION:
             raise RuntimeError("libmambahip.so ABI version mismatch")
     return _lib
 

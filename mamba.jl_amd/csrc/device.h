@@ -23,7 +23,7 @@ struct DBlock {
   double target, beta, scale;
   double width0;         // Slice: scalar width
   const double* width;   // Slice: widths[d] (device) or null when scalar
-  const double* sigl;    // AMM: chol(Sigma) lower, row-major d x d (device)
+  const double* sigl;    // AMM, HMC/MALA: chol(Sigma) lower, row-major d x d (device); HMC/MALA: null = I
   // tune state (device, chain-major)
   double* t_sigma;       // AMWG  [K][DP]
   double* t_accept;      // AMWG  [K][DP]
@@ -35,6 +35,7 @@ struct DBlock {
   uint8_t* t_piv;        // AMM   [K][DP] pivot order
   double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
   double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
+  double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)
 };
 
 struct SweepArgs {

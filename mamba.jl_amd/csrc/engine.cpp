@@ -38,6 +38,7 @@ struct BlockHost {
   // device
   double *sigma = nullptr, *accept = nullptr, *Mv = nullptr, *Mvv = nullptr, *Ls = nullptr;
   double *nuts = nullptr, *nfr = nullptr, *width = nullptr, *sigl_d = nullptr;
+  double* hmc = nullptr;  // HMC/MALA [K][2] epsilon, L
   int32_t *m = nullptr, *flags = nullptr;
   uint8_t* piv = nullptr;
 };
@@ -123,6 +124,8 @@ static int tune_len_of(int kind, int d) {
     case MMB_SAMPLER_AMWG: return 2 + 2 * d;
     case MMB_SAMPLER_AMM: return 4 + 2 * d + 2 * tri(d);
     case MMB_SAMPLER_NUTS: return 9;
+    case MMB_SAMPLER_HMC: return 2;   // [epsilon, L]     (HMCTune, hmc.jl:5-10)
+    case MMB_SAMPLER_MALA: return 1;  // [epsilon]        (MALATune, mala.jl:5-9)
     default: return 0;
   }
 }
@@ -172,9 +175,11 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
       delete e;
       return fail(nullptr, MMB_E_ARG, "logistic: need 1 <= ncoef <= %d, nobs >= 1, prior_sd > 0", MMB_LG_DV);
     }
-    if (spec->nblocks != 1 || spec->blocks[0].sampler != MMB_SAMPLER_NUTS) {
+    const int k0 = spec->blocks[0].sampler;
+    if (spec->nblocks != 1 || !(k0 == MMB_SAMPLER_NUTS || k0 == MMB_SAMPLER_HMC || k0 == MMB_SAMPLER_MALA)) {
       delete e;
-      return fail(nullptr, MMB_E_UNSUPPORTED, "logistic: only the [NUTS(:beta)] scheme is lowered");
+      return fail(nullptr, MMB_E_UNSUPPORTED,
+                  "logistic: only the [NUTS(:beta)], [HMC(:beta, ...)] and [MALA(:beta, ...)] schemes are lowered");
     }
     e->P = spec->ncoef; e->pmon = spec->ncoef; e->VS = MMB_LG_DV; e->DP = MMB_LG_DV; e->TP = 0;
     e->lg_N = spec->nobs; e->lg_p = spec->ncoef; e->lg_rps = mmb_lg_rps(spec->nobs);
@@ -258,6 +263,24 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
           return fail(nullptr, MMB_E_UNSUPPORTED, "NUTS for the rats model is not lowered in this version");
         }
         break;
+      case MMB_SAMPLER_HMC:
+      case MMB_SAMPLER_MALA:  // validate(v) (hmc.jl:33-42, mala.jl:28-37)
+        if (e->model == MMB_MODEL_RATS) {
+          delete e;
+          return fail(nullptr, MMB_E_UNSUPPORTED, "HMC/MALA for the rats model is not lowered in this version");
+        }
+        if (s.ntuning != 0) {
+          if (s.ntuning != d * d) {
+            delete e;
+            return fail(nullptr, MMB_E_ARG, "Sigma dimension differs from variate length %d", d);
+          }
+          h.sigl.resize((size_t)d * d);
+          if (chol_lower(d, s.tuning, h.sigl.data())) {
+            delete e;
+            return fail(nullptr, MMB_E_ARG, "PosDefException: Sigma is not positive definite");
+          }
+        }
+        break;
       default:
         delete e;
         return fail(nullptr, MMB_E_ARG, "unknown sampler kind %d", s.sampler);
@@ -283,10 +306,11 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
 
 static void free_dev(mmb_engine* e) {
   for (auto& h : e->blocks) {
-    void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.nfr, h.width, h.sigl_d, h.m, h.flags, h.piv};
+    void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.nfr, h.width, h.sigl_d, h.hmc, h.m, h.flags,
+                    h.piv};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
-    h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.nfr = h.width = h.sigl_d = nullptr;
+    h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.nfr = h.width = h.sigl_d = h.hmc = nullptr;
     h.m = h.flags = nullptr;
     h.piv = nullptr;
   }
@@ -485,6 +509,7 @@ static int upload_blocks(mmb_engine* e) {
     d.sigl = h.sigl_d;
     d.t_sigma = h.sigma; d.t_accept = h.accept; d.t_m = h.m; d.t_flags = h.flags;
     d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_nuts = h.nuts; d.t_nfr = h.nfr;
+    d.t_hmc = h.hmc;
   }
   if (!e->d_blocks) HIPCHK(e, hipMalloc(&e->d_blocks, MMB_MAX_BLOCKS * sizeof(DBlock)));
   HIPCHK(e, hipMemcpy(e->d_blocks, db.data(), db.size() * sizeof(DBlock), hipMemcpyHostToDevice));
@@ -546,6 +571,15 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
         const size_t fr = (size_t)NutsFrames<Mdl<MMB_MODEL_LINE>::G * Mdl<MMB_MODEL_LINE>::R>::DBL;
         HIPCHK(e, dalloc(&h.nfr, K * fr));
       }
+    } else if (h.spec.sampler == MMB_SAMPLER_HMC || h.spec.sampler == MMB_SAMPLER_MALA) {
+      HIPCHK(e, dalloc(&h.hmc, K * 2));
+      std::vector<double> t(K * 2);
+      for (int64_t k = 0; k < K; ++k) { t[2 * k] = h.spec.epsilon; t[2 * k + 1] = (double)h.spec.nsteps; }
+      HIPCHK(e, hipMemcpy(h.hmc, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+      if (!h.sigl.empty()) {
+        HIPCHK(e, dalloc(&h.sigl_d, (size_t)h.d * h.d));
+        HIPCHK(e, hipMemcpy(h.sigl_d, h.sigl.data(), h.sigl.size() * sizeof(double), hipMemcpyHostToDevice));
+      }
     } else if (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) {
       HIPCHK(e, dalloc(&h.width, h.tuning.size()));
       HIPCHK(e, hipMemcpy(h.width, h.tuning.data(), h.tuning.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -601,6 +635,18 @@ static int iters_per_launch(const mmb_engine* e) {
   return e->model == MMB_MODEL_RATS ? 8 : 64;
 }
 
+template <class T>
+static int d2h(mmb_engine* e, std::vector<T>& h, const T* d, size_t n) {
+  h.resize(n);
+  HIPCHK(e, hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
+  return 0;
+}
+template <class T>
+static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
+  HIPCHK(e, hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
 // Config-4 window: ctl / grad kernel pairs until no chain requests a gradient.  The
 // request count is read back every LG_CHECK steps (pinned host word); surplus pairs after
 // the last chain finished are no-ops (the grad kernel exits on count 0, idle chains return).
@@ -621,7 +667,10 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.target = h.spec.target;
   A.X = e->lg_X; A.Xt = e->lg_Xt; A.y = e->lg_y;
   A.vals = e->d_vals; A.vec = e->lg_vec; A.sc = e->lg_sc; A.iv = e->lg_iv; A.itc = e->lg_itc;
-  A.frames = e->lg_frames; A.tune = h.nuts; A.tm = h.m; A.tflags = h.flags;
+  A.kind = h.spec.sampler;
+  A.frames = e->lg_frames; A.tm = h.m; A.tflags = h.flags;
+  A.tune = A.kind == MMB_SAMPLER_NUTS ? h.nuts : h.hmc;
+  A.sigl = h.sigl_d;
   A.draws = draws;
   A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count;
   A.ngrad = e->lg_ngrad;
@@ -631,8 +680,19 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   e->units = 0;
   e->lg_steps = 0;
   if (a->iters > 0) {
-    // every update needs >= 1 gradient; a tree has <= 2^depth leaves; nutsepsilon <= 4001
-    const int64_t cap = a->iters * ((1LL << MMB_NUTS_MAX_DEPTH) + 2) + 4002 + 4 * LG_CHECK;
+    // every update needs >= 1 gradient; a NUTS tree has <= 2^depth leaves and nutsepsilon
+    // <= 4001; HMC needs L + 1 gradients per update, MALA 2
+    int64_t per = (1LL << MMB_NUTS_MAX_DEPTH) + 2, extra = 4002;
+    if (A.kind != MMB_SAMPLER_NUTS) {
+      std::vector<double> th;
+      int rc = d2h(e, th, h.hmc, e->K * 2);
+      if (rc) return rc;
+      double lmax = 0.0;
+      for (int64_t k = 0; k < e->K; ++k) lmax = std::max(lmax, th[k * 2 + 1]);
+      per = A.kind == MMB_SAMPLER_MALA ? 2 : (int64_t)std::max(lmax, 0.0) + 1;
+      extra = 0;
+    }
+    const int64_t cap = a->iters * per + extra + 4 * LG_CHECK;
     std::vector<hipEvent_t>& ev = e->evpool;
     HIPCHK(e, hipMemsetAsync(e->lg_count, 0, 2 * sizeof(int32_t), e->stream));
     hipError_t st = mmb_lg_launch_ctl(A, 1, 0, e->stream);
@@ -660,7 +720,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (*e->lg_hcount == 0) break;
       }
-      if (s > cap) return fail(e, MMB_E_STATE, "logistic NUTS window did not terminate");
+      if (s > cap) return fail(e, MMB_E_STATE, "logistic window did not terminate");
     }
     e->lg_steps = s;
     if (a->time_kernels) {
@@ -781,17 +841,6 @@ int mmb_get_draws(mmb_engine* e, double* draws) {
 }
 
 // ---------------------------------------------------------------- tune (canonical layout)
-template <class T>
-static int d2h(mmb_engine* e, std::vector<T>& h, const T* d, size_t n) {
-  h.resize(n);
-  HIPCHK(e, hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
-  return 0;
-}
-template <class T>
-static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
-  HIPCHK(e, hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
-  return 0;
-}
 
 int mmb_get_tune(mmb_engine* e, double* tune) {
   if (!e || !tune) return fail(e, MMB_E_ARG, "null argument");
@@ -845,6 +894,11 @@ int mmb_get_tune(mmb_engine* e, double* tune) {
         for (int i = 0; i < 6; ++i) t[2 + i] = nt[k * 8 + i];
         t[8] = (fl[k] & 8) ? 1.0 : 0.0;
       }
+    } else if (h.spec.sampler == MMB_SAMPLER_HMC || h.spec.sampler == MMB_SAMPLER_MALA) {
+      std::vector<double> th;
+      if ((rc = d2h(e, th, h.hmc, K * 2))) return rc;
+      for (int64_t k = 0; k < K; ++k)
+        for (int i = 0; i < h.tune_len; ++i) tune[k * TL + off + i] = th[k * 2 + i];
     }
     off += h.tune_len;
   }
@@ -899,6 +953,14 @@ int mmb_set_tune(mmb_engine* e, const double* tune) {
         for (int i = 0; i < 6; ++i) nt[k * 8 + i] = t[2 + i];
       }
       if ((rc = h2d(e, h.nuts, nt))) return rc;
+    } else if (h.spec.sampler == MMB_SAMPLER_HMC || h.spec.sampler == MMB_SAMPLER_MALA) {
+      std::vector<double> th(K * 2);
+      for (int64_t k = 0; k < K; ++k) {
+        const double* t = tune + k * TL + off;
+        th[k * 2] = t[0];
+        th[k * 2 + 1] = h.tune_len > 1 ? t[1] : (double)h.spec.nsteps;
+      }
+      if ((rc = h2d(e, h.hmc, th))) return rc;
     }
     if ((rc = h2d(e, h.m, m)) || (rc = h2d(e, h.flags, fl))) return rc;
     off += h.tune_len;
@@ -977,6 +1039,8 @@ int mmb_state_bytes(const mmb_engine* e, double* bytes) {
       case MMB_SAMPLER_AMWG: s += 8.0 * h.d * 2 + 4.0 * h.d * 0 + 4.0; break;  // sigma, accept, m
       case MMB_SAMPLER_AMM: s += 8.0 * (h.d + 2.0 * h.T) + 1.0 * h.d + 4.0; break;  // Mv, Mvv, L, piv, m
       case MMB_SAMPLER_NUTS: s += 8.0 * 7 + 4.0; break;
+      case MMB_SAMPLER_HMC: s += 8.0 * 2; break;   // epsilon, L (read only)
+      case MMB_SAMPLER_MALA: s += 8.0; break;
       default: break;
     }
   }

@@ -1,4 +1,4 @@
-// logistic.h — device state of the batched-gradient NUTS engine (BASELINE config 4).
+// logistic.h — device state of the batched-gradient engine (BASELINE config 4: NUTS; also HMC, MALA).
 //
 // Model (build-defined after doc/examples/surgical.jl:14-24):
 //   y[n] ~ Bernoulli(invlogit(X[n,:] beta)),  beta ~ MvNormal(p, prior_sd),  scheme [NUTS(:beta)].
@@ -16,6 +16,7 @@
 #define MMB_LG_NIV 16
 
 struct LgArgs {
+  int32_t kind;            // mmb_sampler_kind of the single block: NUTS, HMC or MALA
   int32_t K, p, N, rps;    // chains, coefficients, rows, rows per sub-range (mmb_lg_rps)
   int32_t Np;              // padded rows = MMB_LG_NG * MMB_LG_NS * rps
   uint32_t chain_offset;
@@ -32,7 +33,8 @@ struct LgArgs {
   int32_t* iv;             // [K][MMB_LG_NIV]
   int64_t* itc;            // [K] last completed iteration
   double* frames;          // [K][NutsFrames<64>::DBL]
-  double* tune;            // [K][8] eps, epsbar, Hbar, mu, alpha, nalpha
+  double* tune;            // NUTS [K][8] eps, epsbar, Hbar, mu, alpha, nalpha | HMC/MALA [K][2] epsilon, L
+  const double* sigl;      // HMC/MALA chol(Sigma) lower row-major p x p, or null (I)
   int32_t* tm;             // [K] m
   int32_t* tflags;         // [K]
   double* draws;           // [n_kept][p][K] or null

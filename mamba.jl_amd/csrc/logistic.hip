@@ -10,6 +10,7 @@
 //                                    GEMM reused directly as B operands of the second
 // as MMB_LG_NG group partials; the next lg_ctl_kernel sums them in group order (no atomics:
 // the summation order is the mmb_math.h spec, restated by oracle/oracle.c).
+#include "hmc.h"
 #include "logistic.h"
 #include "nuts.h"
 
@@ -62,8 +63,8 @@ __device__ __forceinline__ static void lg_store(const LgArgs& A, int c, int lane
 
 // logpdf!(m, x, block) and its gradient at S.x from the range partials (oracle logf_grad):
 // lf = 0 + prior, + sum of range partials if finite; grad = -x/sd^2 + partials, non-finite -> 0.
-__device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, int lane, const Grp<64>& g,
-                                                   NU::St& S) {
+template <class ST>
+__device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, int lane, const Grp<64>& g, ST& S) {
   const bool el = lane < A.p;
   const double x = S.x[0];
   const double sd2 = A.prior_sd * A.prior_sd;
@@ -84,24 +85,17 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   S.lf = lf;
 }
 
-__global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.count[parity ^ 1] = 0;  // next step's counter
-  const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (c >= A.K) return;
-  Grp<64> g;
-  const int lane = g.lane;
-  NU::St S;
-  lg_load(A, c, lane, S);
-  int64_t itc = A.itc[c];
-  if (start) {
-    S.pc = NPC_BEGIN;
-    itc = A.iter0;
+// The per-chain sampler machine driven by lg_ctl_kernel: NUTS (nuts.h) or HMC/MALA (hmc.h).
+struct LgNuts {
+  using St = NU::St;
+  static constexpr int IDLE = NPC_IDLE;
+  __device__ static bool wants(int pc) { return npc_wants_grad(pc); }
+  __device__ static void load(const LgArgs& A, int c, int lane, St& S) { lg_load(A, c, lane, S); }
+  __device__ static void store(const LgArgs& A, int c, int lane, const St& S, int slot, int64_t itc) {
+    lg_store(A, c, lane, S, slot, itc);
   }
-  if (S.pc == NPC_IDLE) return;
-  if (npc_wants_grad(S.pc)) lg_assemble(A, A.iv[(size_t)c * MMB_LG_NIV + 10], lane, g, S);
-  const uint32_t chain = A.chain_offset + (uint32_t)c;
-  for (;;) {
-    const int64_t cur = itc + 1;
+  __device__ static bool advance(const LgArgs& A, St& S, int c, uint32_t chain, int64_t cur, int lane,
+                                 const Grp<64>& g) {
     NU::Env E;
     E.d = A.p;
     E.lane = lane;
@@ -111,12 +105,86 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
     E.ru = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_UNIFORM);
     E.ri = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_INIT);
     E.F = A.frames + (size_t)c * LgFr::DBL;
-    if (NU::advance(S, E, g)) {
+    return NU::advance(S, E, g);
+  }
+};
+
+using HM = Hmc<64, 1>;
+// HMC/MALA state: x = vec[0], p = vec[1], logf0 = sc[0], k0 = sc[1], pc = iv[0], i = iv[1];
+// the gradient is always fresh when a machine resumes, so g is never stored.
+template <bool MALA>
+struct LgHmc {
+  using St = HM::St;
+  static constexpr int IDLE = HPC_DONE + 1;
+  __device__ static bool wants(int pc) { return pc == HPC_G0 || pc == HPC_STEP || pc == HPC_MG1; }
+  __device__ static void load(const LgArgs& A, int c, int lane, St& S) {
+    const double* vb = A.vec + (size_t)c * MMB_LG_NVEC * 64 + lane;
+    S.x[0] = vb[0];
+    S.p[0] = vb[64];
+    S.g[0] = 0.0;
+    S.v[0] = A.vals[(size_t)c * 64 + lane];
+    const double* sc = A.sc + (size_t)c * MMB_LG_NSC;
+    S.logf0 = sc[0];
+    S.k0 = sc[1];
+    const int32_t* iv = A.iv + (size_t)c * MMB_LG_NIV;
+    S.pc = iv[0];
+    S.i = iv[1];
+  }
+  __device__ static void store(const LgArgs& A, int c, int lane, const St& S, int slot, int64_t itc) {
+    double* vb = A.vec + (size_t)c * MMB_LG_NVEC * 64 + lane;
+    vb[0] = S.x[0];
+    vb[64] = S.p[0];
+    A.vals[(size_t)c * 64 + lane] = S.v[0];
+    if (lane == 0) {
+      double* sc = A.sc + (size_t)c * MMB_LG_NSC;
+      sc[0] = S.logf0;
+      sc[1] = S.k0;
+      int32_t* iv = A.iv + (size_t)c * MMB_LG_NIV;
+      iv[0] = S.pc;
+      iv[1] = S.i;
+      iv[10] = slot;
+      A.itc[c] = itc;
+    }
+  }
+  __device__ static bool advance(const LgArgs& A, St& S, int c, uint32_t chain, int64_t cur, int lane,
+                                 const Grp<64>& g) {
+    HM::Env E;
+    E.d = A.p;
+    E.lane = lane;
+    E.eps = A.tune[(size_t)c * 2];
+    E.L = (int)A.tune[(size_t)c * 2 + 1];
+    E.sigl = A.sigl;
+    E.rn = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_NORMAL);
+    E.ru = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_UNIFORM);
+    return MALA ? HM::advance_mala(S, E, g) : HM::advance_hmc(S, E, g);
+  }
+};
+
+template <class MC>
+__global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) A.count[parity ^ 1] = 0;  // next step's counter
+  const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (c >= A.K) return;
+  Grp<64> g;
+  const int lane = g.lane;
+  typename MC::St S;
+  MC::load(A, c, lane, S);
+  int64_t itc = A.itc[c];
+  if (start) {
+    S.pc = 0;  // NPC_BEGIN / HPC_BEGIN
+    itc = A.iter0;
+  }
+  if (S.pc == MC::IDLE) return;
+  if (MC::wants(S.pc)) lg_assemble(A, A.iv[(size_t)c * MMB_LG_NIV + 10], lane, g, S);
+  const uint32_t chain = A.chain_offset + (uint32_t)c;
+  for (;;) {
+    const int64_t cur = itc + 1;
+    if (MC::advance(A, S, c, chain, cur, lane, g)) {
       int slot = 0;
       if (lane == 0) slot = atomicAdd(&A.count[parity], 1);
       slot = __shfl(slot, 0, 64);
       A.pos[(size_t)slot * 64 + lane] = S.x[0];
-      lg_store(A, c, lane, S, slot, itc);
+      MC::store(A, c, lane, S, slot, itc);
       return;
     }
     itc = cur;  // mcmc_worker! keep rule (mcmc.jl:76): sim[i,:,1] = unlist(m, true)
@@ -125,11 +193,11 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
       A.draws[(size_t)(row * A.p + lane) * A.K + c] = S.v[0];
     }
     if (itc >= A.it_end) {
-      S.pc = NPC_IDLE;
-      lg_store(A, c, lane, S, 0, itc);
+      S.pc = MC::IDLE;
+      MC::store(A, c, lane, S, 0, itc);
       return;
     }
-    S.pc = NPC_BEGIN;
+    S.pc = 0;
   }
 }
 
@@ -227,7 +295,13 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
 }
 
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st) {
-  hipLaunchKernelGGL(lg_ctl_kernel, dim3((A.K + 3) / 4), dim3(256), 0, st, A, start, parity);
+  const dim3 grid((A.K + 3) / 4), blk(256);
+  if (A.kind == MMB_SAMPLER_HMC)
+    hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<false>>, grid, blk, 0, st, A, start, parity);
+  else if (A.kind == MMB_SAMPLER_MALA)
+    hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<true>>, grid, blk, 0, st, A, start, parity);
+  else
+    hipLaunchKernelGGL(lg_ctl_kernel<LgNuts>, grid, blk, 0, st, A, start, parity);
   return hipGetLastError();
 }
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {

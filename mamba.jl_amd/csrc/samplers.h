@@ -4,6 +4,7 @@
 // is mirrored draw for draw by oracle/oracle.c.
 #pragma once
 #include "models.h"
+#include "hmc.h"
 #include "nuts.h"
 
 template <class M>
@@ -606,6 +607,33 @@ struct Smp {
       tw[4] = S.t_alpha; tw[5] = S.t_nalpha;
       B.t_m[c] = S.t_m;
       B.t_flags[c] = S.t_flags;
+    }
+    M::relist(B, s, g, S.v);
+  }
+
+  // ---------------------------------------------------------------- HMC / MALA
+  // sample!(v::HMCVariate) (hmc.jl:72-111) / sample!(v::MALAVariate) (mala.jl:67-90), hmc.h
+  // machines with the model gradient computed inline; tune (epsilon, L) is per chain.
+  template <bool MALA>
+  __device__ __forceinline__ static void hmc(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,
+                                             const mmb_rng& ru, St& s, const Grp<G>& g) {
+    using HM = Hmc<G, R>;
+    typename HM::St S;
+    typename HM::Env E;
+    const double* th = B.t_hmc + (size_t)c * 2;
+    E.d = B.d;
+    E.lane = g.lane;
+    E.eps = th[0];
+    E.L = (int)th[1];
+    E.sigl = B.sigl;
+    E.rn = rn;
+    E.ru = ru;
+    M::unlist(B, s, g.lane, S.v);
+    S.pc = HPC_BEGIN;
+    if (MALA) {
+      while (HM::advance_mala(S, E, g)) S.lf = M::logf_grad(A, B, s, S.x, S.g);
+    } else {
+      while (HM::advance_hmc(S, E, g)) S.lf = M::logf_grad(A, B, s, S.x, S.g);
     }
     M::relist(B, s, g, S.v);
   }

@@ -79,6 +79,12 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
         case MMB_SAMPLER_NUTS:
           if constexpr ((KINDS >> MMB_SAMPLER_NUTS) & 1u) S::nuts(A, B, c, it, b, s, g);
           break;
+        case MMB_SAMPLER_HMC:
+          if constexpr ((KINDS >> MMB_SAMPLER_HMC) & 1u) S::template hmc<false>(A, B, c, rn, ru, s, g);
+          break;
+        case MMB_SAMPLER_MALA:
+          if constexpr ((KINDS >> MMB_SAMPLER_MALA) & 1u) S::template hmc<true>(A, B, c, rn, ru, s, g);
+          break;
         case MMB_SAMPLER_GIBBS: if constexpr ((KINDS >> MMB_SAMPLER_GIBBS) & 1u) {
           const mmb_rng gn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_N);
           const mmb_rng gu = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_U);
@@ -114,7 +120,8 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
 
 constexpr unsigned K_ALL = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_AMM) |
                          (1u << MMB_SAMPLER_SLICE) | (1u << MMB_SAMPLER_GIBBS);
-constexpr unsigned K_ALL_NUTS = K_ALL | (1u << MMB_SAMPLER_NUTS);
+constexpr unsigned K_GRAD = (1u << MMB_SAMPLER_NUTS) | (1u << MMB_SAMPLER_HMC) | (1u << MMB_SAMPLER_MALA);
+constexpr unsigned K_ALL_GRAD = K_ALL | K_GRAD;
 constexpr unsigned K_GIBBS_AMM = (1u << MMB_SAMPLER_AMM) | (1u << MMB_SAMPLER_GIBBS);
 constexpr unsigned K_SLICE_AMWG = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_SLICE);
 
@@ -140,7 +147,7 @@ hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipSt
     return launch<MMB_MODEL_RATS, K_ALL>(A, st, TB);
   }
   if (model == MMB_MODEL_LINE) {
-    if (kinds & (1u << MMB_SAMPLER_NUTS)) return launch<MMB_MODEL_LINE, K_ALL_NUTS>(A, st, 64);
+    if (kinds & K_GRAD) return launch<MMB_MODEL_LINE, K_ALL_GRAD>(A, st, 64);
     return launch<MMB_MODEL_LINE, K_ALL>(A, st, 64);
   }
   return hipErrorInvalidValue;

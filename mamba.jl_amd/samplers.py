@@ -8,6 +8,8 @@ Argument meaning, defaults and validation errors follow the reference:
   AMM(params, Sigma; adapt=:all, beta=0.05, scale=2.38)        src/samplers/amm.jl:45-59
   NUTS(params; dtype=:forward, target=0.6)                     src/samplers/nuts.jl:47-56
   Slice(params, width, Univariate|Multivariate; transform=false) src/samplers/slice.jl:47-58
+  HMC(params, epsilon, L[, Sigma]; dtype=:forward)            src/samplers/hmc.jl:47-65
+  MALA(params, epsilon[, Sigma]; dtype=:forward)              src/samplers/mala.jl:43-58
   Gibbs(params)  -- a user `Sampler(params, f)` whose f is the node's conjugate full
                     conditional (doc/tutorial/line.jl:168-186); lowered per model.
 """
@@ -48,6 +50,8 @@ class Sampler:
         self.target = float(kw.pop("target", 0.44))
         self.beta = float(kw.pop("beta", 0.05))
         self.scale = float(kw.pop("scale", 2.38))
+        self.epsilon = float(kw.pop("epsilon", 0.0))
+        self.nsteps = int(kw.pop("nsteps", 0))
         if kw:
             raise ArgumentError(f"unsupported sampler arguments {sorted(kw)}")
         self.targets = []
@@ -61,9 +65,11 @@ class Sampler:
             raise ArgumentError(f"Sigma dimension differs from variate length {dim}")
         if self.kind == abi.MMB_SAMPLER_SLICE and not (t.size == 1 or t.size == dim):
             raise ArgumentError(f"length(width) differs from variate length {dim}")
+        if self.kind in (abi.MMB_SAMPLER_HMC, abi.MMB_SAMPLER_MALA) and t is not None and t.size != dim * dim:
+            raise ArgumentError(f"Sigma dimension differs from variate length {dim}")
 
     def __repr__(self):
-        names = {1: "AMWG", 2: "AMM", 3: "NUTS", 4: "Slice", 5: "Gibbs"}
+        names = {1: "AMWG", 2: "AMM", 3: "NUTS", 4: "Slice", 5: "Gibbs", 6: "HMC", 7: "MALA"}
         return f"{names[self.kind]}({self.params})"
 
 
@@ -82,11 +88,39 @@ def AMM(params, Sigma, adapt="all", beta=0.05, scale=2.38):
 
 
 def NUTS(params, dtype="forward", target=0.6):
+    _dtype(dtype)
+    return Sampler(params, abi.MMB_SAMPLER_NUTS, abi.MMB_ADAPT_BURNIN, None, target=target)
+
+
+def _dtype(dtype):
     # dtype selects Calculus' finite-difference scheme in the reference; the lowered
     # models supply analytic gradients, so it is accepted and ignored.
     if str(dtype).lstrip(":") not in ("forward", "central", "complex"):
         raise ArgumentError(f"unsupported dtype {dtype}")
-    return Sampler(params, abi.MMB_SAMPLER_NUTS, abi.MMB_ADAPT_BURNIN, None, target=target)
+
+
+def _sigma(Sigma):
+    if Sigma is None:
+        return None  # SigmaL = I (UniformScaling)
+    S = np.asarray(Sigma, dtype=np.float64)
+    if S.ndim != 2 or S.shape[0] != S.shape[1]:
+        raise ArgumentError("Sigma must be a square matrix")
+    return S.ravel(order="F")
+
+
+def HMC(params, epsilon, L, Sigma=None, dtype="forward"):
+    """HMC(params, epsilon, L[, Sigma]; dtype) -- hmc.jl:47-55; tune [epsilon, L] (HMCTune)."""
+    _dtype(dtype)
+    if int(L) != L:
+        raise ArgumentError("L must be an integer")
+    return Sampler(params, abi.MMB_SAMPLER_HMC, abi.MMB_ADAPT_NONE, _sigma(Sigma), epsilon=epsilon,
+                   nsteps=int(L))
+
+
+def MALA(params, epsilon, Sigma=None, dtype="forward"):
+    """MALA(params, epsilon[, Sigma]; dtype) -- mala.jl:43-51; tune [epsilon] (MALATune)."""
+    _dtype(dtype)
+    return Sampler(params, abi.MMB_SAMPLER_MALA, abi.MMB_ADAPT_NONE, _sigma(Sigma), epsilon=epsilon)
 
 
 def Slice(params, width, form=Multivariate, transform=False):

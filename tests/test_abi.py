@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(mamba):
     assert len(syms) >= 20
     missing = [s for s in syms if s not in exported]
     assert not missing, missing
-    assert lib.mmb_abi_version() == 1
+    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 2
 
 
 def test_struct_layout_matches_header(mamba):
@@ -34,9 +34,10 @@ def test_struct_layout_matches_header(mamba):
 #include <stddef.h>
 #include <stdio.h>
 #include "mamba_hip.h"
-int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(mmb_block_spec), sizeof(mmb_model_spec),
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(mmb_block_spec), sizeof(mmb_model_spec),
  sizeof(mmb_run_args), offsetof(mmb_block_spec, tuning), offsetof(mmb_model_spec, prior_sd),
- offsetof(mmb_run_args, keep_device)); return 0;}
+ offsetof(mmb_run_args, keep_device), offsetof(mmb_block_spec, epsilon), offsetof(mmb_block_spec, nsteps));
+ return 0;}
 """
     d = "/tmp/mmb_layout"
     os.makedirs(d, exist_ok=True)
@@ -45,7 +46,8 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(mmb_block_spec), size
     got = list(map(int, subprocess.check_output([f"{d}/t"]).split()))
     a = mamba.abi
     want = [C.sizeof(a.BlockSpec), C.sizeof(a.ModelSpec), C.sizeof(a.RunArgs), a.BlockSpec.tuning.offset,
-            a.ModelSpec.prior_sd.offset, a.RunArgs.keep_device.offset]
+            a.ModelSpec.prior_sd.offset, a.RunArgs.keep_device.offset, a.BlockSpec.epsilon.offset,
+            a.BlockSpec.nsteps.offset]
     assert got == want
 
 
@@ -63,6 +65,18 @@ def test_create_validates_before_touching_the_device(mamba):
     assert lib.mmb_create(C.byref(r.spec()), 0, C.byref(h)) == -2
     r.setsamplers([mamba.Slice(["alpha", "mu_alpha"], 1.0)])   # mixed vector/scalar block
     assert lib.mmb_create(C.byref(r.spec()), 0, C.byref(h)) == -2
+    r.setsamplers([mamba.HMC("alpha", 0.1, 5)])                # HMC not lowered for rats
+    assert lib.mmb_create(C.byref(r.spec()), 0, C.byref(h)) == -2
+    m.setsamplers([mamba.MALA(["beta", "s2"], 0.1, np.eye(3))])
+    sp = m.spec()
+    sp.blocks[0].ntuning = 4                                   # Sigma of the wrong size
+    assert lib.mmb_create(C.byref(sp), 0, C.byref(h)) == -1
+    assert b"Sigma dimension" in lib.mmb_last_error(None)
+    m.setsamplers([mamba.HMC(["beta", "s2"], 0.1, 3, -np.eye(3))])
+    assert lib.mmb_create(C.byref(m.spec()), 0, C.byref(h)) == -1   # cholfact: not PD
+    lg = mamba.logistic(10, 3)
+    lg.setsamplers([mamba.AMWG("beta", 1.0)])                  # logistic lowers NUTS/HMC/MALA only
+    assert lib.mmb_create(C.byref(lg.spec()), 0, C.byref(h)) == -2
 
 
 def test_python_argument_errors(mamba):
@@ -73,6 +87,10 @@ def test_python_argument_errors(mamba):
         m.setsamplers([mamba.AMWG("alpha", [1.0, 2.0])])
     with pytest.raises(mamba.ArgumentError, match="Sigma dimension"):
         m.setsamplers([mamba.AMM("alpha", np.eye(3))])
+    with pytest.raises(mamba.ArgumentError, match="Sigma dimension"):
+        mamba.line().setsamplers([mamba.HMC(["beta", "s2"], 0.1, 10, np.eye(2))])
+    with pytest.raises(mamba.ArgumentError, match="unsupported dtype"):
+        mamba.MALA("beta", 0.1, dtype="backward")
     with pytest.raises(mamba.ArgumentError, match="burnin is greater"):
         mamba.mcmc(m.setsamplers([mamba.Gibbs("s2_c")]), mamba.model.RATS_DATA, mamba.model.RATS_INITS, 10,
                    burnin=10)

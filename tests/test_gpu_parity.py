@@ -43,6 +43,13 @@ LINE_SCHEMES = {
     "amwg_slice": lambda M: [M.AMWG("beta", 1.0), M.Slice("s2", 3.0, transform=True)],
     "nuts": lambda M: [M.NUTS(["beta", "s2"])],
     "nuts_slice": lambda M: [M.NUTS("beta"), M.Slice("s2", 3.0)],        # doc/tutorial/line.jl:53-56
+    "hmc": lambda M: [M.HMC(["beta", "s2"], 0.05, 8)],
+    "hmc_sigma_slice": lambda M: [M.HMC("beta", 0.1, 5, np.array([[1.6, -0.45], [-0.45, 0.15]])),
+                                  M.Slice("s2", 3.0)],
+    "hmc_l0": lambda M: [M.HMC(["beta", "s2"], 0.05, 0)],
+    "mala": lambda M: [M.MALA(["beta", "s2"], 0.01)],
+    "mala_sigma_gibbs": lambda M: [M.MALA("beta", 0.3, np.array([[1.6, -0.45], [-0.45, 0.15]])),
+                                   M.Gibbs("s2")],
 }
 
 
@@ -129,11 +136,41 @@ def test_mcmc_api_and_full_size_properties(mamba):
     assert abs(mb - 6.183) < 0.02 and abs(a0 - 106.63) < 0.5, (mb, a0)
 
 
-def logistic(mamba, nobs, ncoef):
+def logistic(mamba, nobs, ncoef, scheme=None):
     data, bt = mamba.model.logistic_data(nobs, ncoef)
     m = mamba.logistic(nobs, ncoef, 10.0)
     m.setinputs(data)
-    return m.setsamplers([mamba.NUTS("beta")]), bt
+    return m.setsamplers(scheme or [mamba.NUTS("beta")]), bt
+
+
+def _spd(p, seed, a, b):
+    A = np.random.default_rng(seed).normal(0.0, 1.0, (p, p + 4))
+    return (A @ A.T) / (p + 4) * a + b * np.eye(p)
+
+
+LOGISTIC_GRAD_SCHEMES = {
+    "hmc": lambda M, p: [M.HMC("beta", 0.01, 7)],
+    "hmc_sigma": lambda M, p: [M.HMC("beta", 0.01, 4, _spd(p, 1, 0.2, 1.0))],   # near I (unit-mass leapfrog)
+    "mala": lambda M, p: [M.MALA("beta", 2e-4)],
+    "mala_sigma": lambda M, p: [M.MALA("beta", 0.5, _spd(p, 2, 1e-3, 1e-4))],
+}
+
+
+@pytest.mark.parametrize("name", sorted(LOGISTIC_GRAD_SCHEMES))
+def test_logistic_hmc_mala_parity(mamba, oracle, name):
+    """HMC / MALA (hmc.jl:72-111, mala.jl:67-90) on the batched MFMA gradient engine:
+    bit-exact against the oracle (same gradient summation spec as NUTS)."""
+    m, _ = logistic(mamba, 1000, 50, LOGISTIC_GRAD_SCHEMES[name](mamba, 50))
+    K = 100
+    init = np.random.default_rng(9).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 25, 5, 1)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+    # moves happened (not all rejected) and gradient counts are exact
+    assert (np.abs(np.diff(dg, axis=0)).sum(axis=1) > 0).mean() > 0.2
+    per = 8 if name == "hmc" else 5 if name == "hmc_sigma" else 2
+    assert eng.grad_evals() == 25 * K * per
 
 
 def test_logistic_nuts_parity(mamba, oracle):

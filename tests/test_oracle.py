@@ -184,6 +184,34 @@ def test_line_nuts_gaussian_conditional(mamba, oracle):
         assert abs(d[:, j, :].std() / np.sqrt(C[j, j]) - 1) < 0.03
 
 
+C_LINE = np.array([[1.6, -0.45], [-0.45, 0.15]])   # ~ Cov(beta | s2 = 1.5)
+# HMC keeps the reference's unit-mass leapfrog (x += eps p) whatever Sigma is, while p ~ N(0, Sigma)
+# and K = p' Sigma^-1 p / 2 (hmc.jl:79-104): valid, but only efficient for Sigma near I.
+S_HMC = np.array([[1.0, 0.2], [0.2, 0.5]])
+
+
+@pytest.mark.parametrize("scheme", ["hmc", "hmc_sigma", "mala", "mala_sigma"])
+def test_line_hmc_mala_gaussian_conditional(mamba, oracle, scheme):
+    """HMC (hmc.jl:72-111) and MALA (mala.jl:67-90), with SigmaL = I and with a Sigma, on
+    the exact Gaussian beta | s2 (as test_line_nuts_gaussian_conditional)."""
+    S = {"hmc": mamba.HMC("beta", 0.1, 16), "hmc_sigma": mamba.HMC("beta", 0.1, 16, S_HMC),
+         "mala": mamba.MALA("beta", 0.02), "mala_sigma": mamba.MALA("beta", 0.6, C_LINE)}[scheme]
+    m = line_model(mamba, [S])
+    init = np.zeros((64, 3))
+    init[:, 2] = 1.5
+    st = oracle.new_state(m, init)
+    d = oracle.run(m, st, 8000, burnin=1000, thin=1, seed=5, nthreads=8)
+    X = np.c_[np.ones(5), np.arange(1.0, 6.0)]
+    y = np.array([1.0, 3, 3, 3, 5])
+    C = np.linalg.inv(X.T @ X / 1.5 + np.eye(2) / 1000.0)
+    mu = C @ (X.T @ y / 1.5)
+    for j in range(2):
+        ok, info = _mcse_ok(d[:, j, :], mu[j])
+        assert ok, (scheme, j, info)
+        assert abs(d[:, j, :].std() / np.sqrt(C[j, j]) - 1) < 0.04, (scheme, j, d[:, j, :].std())
+    np.testing.assert_array_equal(st["tune"][:, 0], S.epsilon)           # not adapted
+
+
 def test_rats_reference_scheme_statistical(mamba, oracle):
     """rats.jl:112-116 scheme vs the published rats.rst:37-52 summaries."""
     pub = load("rats_published.json")
@@ -231,6 +259,29 @@ def test_logistic_nuts_posterior_laplace(mamba, oracle):
     sd = np.sqrt(np.diag(np.linalg.inv(H)))
     st = oracle.new_state(m, np.zeros((32, p)))
     d = oracle.run(m, st, 600, burnin=200, thin=1, seed=11, model_burnin=200, nthreads=8)
+    mean = d.mean(axis=(0, 2))
+    assert np.all(np.abs(mean - b) < 0.15 * sd), (mean, b, sd)
+    assert np.all(np.abs(d.std(axis=(0, 2)) / sd - 1) < 0.1), (d.std(axis=(0, 2)), sd)
+
+
+@pytest.mark.parametrize("scheme", ["hmc", "mala"])
+def test_logistic_hmc_mala_posterior_laplace(mamba, oracle, scheme):
+    """HMC / MALA on the logistic model (N=2000, p=6) against the Laplace approximation."""
+    N, p = 2000, 6
+    data, _ = mamba.model.logistic_data(N, p)
+    X, y = data["X"], data["y"]
+    m = mamba.logistic(N, p, 10.0)
+    m.setinputs(data)
+    m.setsamplers([mamba.HMC("beta", 0.02, 8) if scheme == "hmc" else mamba.MALA("beta", 1.5e-3)])
+    b = np.zeros(p)
+    for _ in range(50):
+        mu = 1.0 / (1.0 + np.exp(-(X @ b)))
+        g = X.T @ (y - mu) - b / 100.0
+        H = (X * (mu * (1 - mu))[:, None]).T @ X + np.eye(p) / 100.0
+        b = b + np.linalg.solve(H, g)
+    sd = np.sqrt(np.diag(np.linalg.inv(H)))
+    st = oracle.new_state(m, np.tile(b, (32, 1)))
+    d = oracle.run(m, st, 1200 if scheme == "mala" else 600, burnin=200, thin=1, seed=12, nthreads=8)
     mean = d.mean(axis=(0, 2))
     assert np.all(np.abs(mean - b) < 0.15 * sd), (mean, b, sd)
     assert np.all(np.abs(d.std(axis=(0, 2)) / sd - 1) < 0.1), (d.std(axis=(0, 2)), sd)
