@@ -265,6 +265,136 @@ struct Smp {
     return rank;
   }
 
+  // Exact pivot choice for the rare cases the fast search hands over (ties of the high
+  // words, NaN candidates): replays dpstf2's position swaps from the pivot history and
+  // takes the first maximum in position order.  Out of line: it is shared by every
+  // unrolled step instead of being inlined 30 times.
+  __device__ __forceinline__ static int pivot_exact(double dl, bool done, const int* pks, int j,
+                                                              int d, int* perm, double* val) {
+    const int lane = (int)(threadIdx.x & (G - 1));
+    if (lane == 0) {
+      for (int t = 0; t < d; ++t) perm[t] = t;
+      for (int k = 0; k < j; ++k) {
+        int q = pks[k], qpos = k;
+        for (int t = k; t < d; ++t) if (perm[t] == q) qpos = t;
+        int tmp = perm[k]; perm[k] = q; perm[qpos] = tmp;
+      }
+    }
+    grp_sync();
+    int mypos = 0x7fffffff;
+    for (int t = j; t < d; ++t) if (perm[t] == lane) mypos = t;
+    grp_sync();
+    double key = done ? -__builtin_inf()
+                      : (isnan(dl) ? (mypos == j ? __builtin_inf() : -__builtin_inf()) : dl);
+    int pi = (done ? 0x7fff : mypos) << 16 | lane;
+    Grp<G> g;
+    g.argmax(key, pi);
+    const int p = pi & 0xffff;
+    *val = g.bcast(dl, p);
+    return p;
+  }
+
+  // group max of an int over the 32 lanes: four row stages (DPP folded into v_max_i32)
+  // and one permlane16 swap whose two outputs are the two rows of each half
+  __device__ __forceinline__ static int gmax_i32(int x) {
+    x = max(x, dpp_i<MMB_DPP_XOR1>(x));
+    x = max(x, dpp_i<MMB_DPP_XOR2>(x));
+    x = max(x, dpp_i<MMB_DPP_HMIRROR>(x));
+    x = max(x, dpp_i<MMB_DPP_MIRROR>(x));
+    auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    return max((int)r[0], (int)r[1]);
+  }
+
+  // pchol for 32-lane groups with one row per lane (rats), same results as pchol():
+  // * every lane computes sqrt / reciprocal of its own remaining diagonal while the pivot
+  //   is searched (the pivot lane's pair is exactly sqrt(val), 1/sqrt(val)); the pivot lane
+  //   publishes its reciprocal through LDS together with its factor row;
+  // * the search reduces the high words of the positive candidates as int32 (one DPP
+  //   max per stage); a unique maximal high word is the unique maximum.  High-word ties
+  //   and NaN candidates go to pivot_exact (dpstf2's first maximum in position order).
+  // Measured (rats sweep, 16384 chains): 0.255 -> 0.248 ms; the factorization is bound by
+  // its f64 work per step (sqrt, reciprocal, dot product), not by the pivot search.
+  __device__ __forceinline__ static int pchol32(int d, double* mat, double* prow, int* pks, const Grp<G>& g) {
+    constexpr int RI = DMAX;  // prow[RI]: the pivot's reciprocal
+    const int lane = g.lane;
+    const bool hi_half = (threadIdx.x & 32) != 0;
+    const bool inb = lane < d;
+    const double diag0 = inb ? mat[mmb_tri(lane) + lane] : 0.0;
+    double work = 0.0;
+    double Lrow[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
+    bool done = !inb;
+    int rank = d;
+    bool live = true;
+#pragma unroll
+    for (int j = 0; j < DMAX; ++j) {
+      if (live && j < d) {
+        const double dl = diag0 - work;
+        const double ajj = sqrt(dl);
+        const double rinv = 1.0 / ajj;
+        // key: high word of a positive candidate, INT_MAX for a NaN candidate, else -1
+        const int hiw = (int)(mmb_d2u(dl) >> 32);
+        const int key = done ? -1 : (isnan(dl) ? 0x7fffffff : (dl > 0.0 ? hiw : -1));
+        const int m = gmax_i32(key);
+        const uint32_t win = (uint32_t)(__ballot(key == m) >> (threadIdx.x & 32));
+        int p = __builtin_ctz(win | 0x80000000u);
+        bool pos = m >= 0;
+        if (!(m < 0 || (m != 0x7fffffff && __builtin_popcount(win) == 1))) {
+          double val;
+          p = pivot_exact(dl, done, pks, j, d, (int*)prow, &val);
+          pos = val > 0.0;
+        }
+        if (!pos) {
+          rank = j;
+          live = false;
+        } else {
+          if (lane == 0) pks[j] = p;
+          const bool piv = lane == p;
+          if (piv) {
+#pragma unroll
+            for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
+            if (j & 1) prow[j - 1] = Lrow[j - 1];
+            prow[RI] = rinv;
+          }
+          grp_sync();
+          if (piv) Lrow[j] = ajj;
+          done = done || piv;
+          if (!done) {
+            double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+            for (int k = 0; k + 1 < j; k += 2) {
+              const double2 pp = *(const double2*)(prow + k);
+              t0 = fma(Lrow[k], pp.x, t0);
+              t1 = fma(Lrow[k + 1], pp.y, t1);
+            }
+            if (j & 1) t0 = fma(Lrow[j - 1], prow[j - 1], t0);
+            const double lij = (mat[mmb_slot(lane, p)] - (t0 + t1)) * prow[RI];
+            Lrow[j] = lij;
+            work = work + lij * lij;
+          }
+          grp_sync();
+        }
+      }
+    }
+    if (rank == d && inb) {  // write the factor back in slot form
+      bool before = true;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        if (k < d) {
+          const int q = pks[k];
+          if (q == lane) {
+            mat[mmb_tri(lane) + lane] = Lrow[k];
+            before = false;
+          } else if (before) {
+            mat[mmb_slot(lane, q)] = Lrow[k];
+          }
+        }
+      }
+    }
+    return rank;
+  }
+
   // (i, k) of packed slot s = tri(i) + k: float square root estimate, integer correction
   __device__ __forceinline__ static void slot_ik(int s, int& i, int& k) {
     int ii = (int)((sqrtf((float)(8 * s + 1)) - 1.0f) * 0.5f);
@@ -466,7 +596,12 @@ struct Smp {
 #ifdef MMB_EXP_NOPCHOL
       int rank = d;  // timing experiment only
 #else
-      int rank = pchol(d, mat, (double*)ia, pks, g);
+      int rank;
+#ifndef MMB_PCHOL_GENERIC
+      if constexpr (G == 32 && R == 1) rank = pchol32(d, mat, (double*)ia, pks, g);
+      else
+#endif
+        rank = pchol(d, mat, (double*)ia, pks, g);
 #endif
       grp_sync();
       MMB_PROF_MARK(5, g.lane)
