@@ -202,16 +202,26 @@ struct Mdl<MMB_MODEL_RATS> {
     return lp;
     (void)NEG;
   }
-  // conjugate full conditionals (Gibbs_s2_c, Gibbs_mu_*, Gibbs_s2_*)
+  // The random draw of a conjugate block does not depend on the chain state: a Gamma(a)
+  // variate for the s2 blocks (rand(InverseGamma(a, b)) = b / G, shape a fixed by the
+  // model), a standard normal for the mu blocks.  The sweep kernel draws them for all
+  // blocks of an iteration at once, one block per lane (predraw), and passes each block
+  // its value.  Returns 1 (gamma, shape *a) or 2 (normal).
+  __device__ __forceinline__ static int gibbs_draw_kind(const DBlock& B, double* a) {
+    const int n = B.nodes[0];
+    if (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_MU_BETA) { *a = 0.0; return 2; }
+    *a = n == MMB_RATS_S2_C ? 150.0 / 2.0 + 0.001 : 30.0 / 2.0 + 0.001;
+    return 1;
+  }
+  // conjugate full conditionals (Gibbs_s2_c, Gibbs_mu_*, Gibbs_s2_*);
+  // `draw` is the block's predrawn Gamma / normal variate (gibbs_draw_kind)
   __device__ __forceinline__ static void gibbs(const SweepArgs& A, const DBlock& B, St& s, const Lc& l,
-                               const Grp<G>& g, const mmb_rng* rn, const mmb_rng* gn,
-                               const mmb_rng* gu) {
+                               const Grp<G>& g, const mmb_rng*, const mmb_rng*, const mmb_rng*, double draw) {
     int n = B.nodes[0];
-    uint32_t kn = 0, ku = 0;
     if (n == MMB_RATS_S2_C) {
       double ss = g.sum(ssr_lane(A, l, s.a, s.b, g.lane));
-      double a = 150.0 / 2.0 + 0.001, b = ss / 2.0 + 0.001;
-      s.s2c = b / mmb_gamma_mt(a, gn, gu, &kn, &ku);
+      double b = ss / 2.0 + 0.001;
+      s.s2c = b / draw;
     } else if (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_MU_BETA) {
       const bool al = n == MMB_RATS_MU_ALPHA;
       double sum = g.sum(g.lane < 30 ? blend(al, s.a, s.b) : 0.0);
@@ -219,7 +229,7 @@ struct Mdl<MMB_MODEL_RATS> {
       double var0 = 1000.0 * 1000.0;
       double vv = 1.0 / (30.0 / s2 + 1.0 / var0);
       double mean = vv * (sum / s2 + 0.0 / var0);
-      double v = mean + sqrt(vv) * mmb_normal(rn, 0u);
+      double v = mean + sqrt(vv) * draw;
       s.mua = blend(al, v, s.mua);
       s.mub = blend(al, s.mub, v);
     } else {
@@ -227,7 +237,7 @@ struct Mdl<MMB_MODEL_RATS> {
       double mu = blend(al, s.mua, s.mub);
       double r = blend(al, s.a, s.b) - mu;
       double ss = g.sum(g.lane < 30 ? r * r : 0.0);
-      double v = (ss / 2.0 + 0.001) / mmb_gamma_mt(30.0 / 2.0 + 0.001, gn, gu, &kn, &ku);
+      double v = (ss / 2.0 + 0.001) / draw;
       s.s2a = blend(al, v, s.s2a);
       s.s2b = blend(al, s.s2b, v);
     }
@@ -347,9 +357,10 @@ struct Mdl<MMB_MODEL_LINE> {
       if (!isfinite(gr[k])) gr[k] = 0.0;
     return lp;
   }
+  __device__ __forceinline__ static int gibbs_draw_kind(const DBlock&, double* a) { *a = 0.0; return 0; }
   __device__ __forceinline__ static void gibbs(const SweepArgs& A, const DBlock& B, St& s, const Lc&,
                                const Grp<G>&, const mmb_rng* rn, const mmb_rng* gn,
-                               const mmb_rng* gu) {
+                               const mmb_rng* gu, double) {
     if (B.nodes[0] == MMB_LINE_BETA) {  // line.jl:168-177
       double s2 = s.v[2];
       double sb = sqrt(1000.0);

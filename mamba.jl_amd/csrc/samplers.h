@@ -14,6 +14,61 @@ struct Smp {
   using St = typename M::St;
   using Lc = typename M::Lc;
 
+  // ---------------------------------------------------------------- per-iteration draws
+  // Variates that do not depend on the chain state, drawn for every block of an iteration
+  // at once with one block per lane (32-lane groups): lane b holds block b's Gibbs variate
+  // (Mdl::gibbs_draw_kind: Gamma(a) by Marsaglia-Tsang or a standard normal) or its AMM
+  // accept uniform.  Same substreams, counters and operations as the per-block draws
+  // (mmb_gamma_mt is replayed in full whenever its first attempt does not accept), so the
+  // values are bit-identical to drawing them inside the blocks.
+  __device__ __forceinline__ static double predraw(const SweepArgs& A, uint32_t chain, int64_t it,
+                                                   const Grp<G>& g) {
+    int kind = 0;  // 0 none, 1 Gamma(a), 2 normal, 3 uniform
+    double a = 0.0;
+    for (int b = 0; b < A.nb; ++b) {
+      const DBlock& B = mmb_block(A.blocks, b);
+      double ab = 0.0;
+      int k = 0;
+      if (B.kind == MMB_SAMPLER_GIBBS) k = M::gibbs_draw_kind(B, &ab);
+      else if (B.kind == MMB_SAMPLER_AMM) k = 3;
+      kind = g.lane == b ? k : kind;
+      a = g.lane == b ? ab : a;
+    }
+    const uint32_t b = (uint32_t)g.lane;
+    const mmb_rng rn = mmb_rng_make(A.seed, chain, (uint32_t)it, b, kind == 1 ? MMB_SUB_GAMMA_N : MMB_SUB_NORMAL);
+    const mmb_rng ru = mmb_rng_make(A.seed, chain, (uint32_t)it, b, kind == 1 ? MMB_SUB_GAMMA_U : MMB_SUB_UNIFORM);
+    const double x = mmb_normal(&rn, 0u);
+    const double u = mmb_uniform(&ru, 0u);
+    if (kind != 1) return kind == 2 ? x : u;
+    // mmb_gamma_mt's first attempt (normal #0, uniform #0)
+    const double d = a - 1.0 / 3.0;
+    const double c = 1.0 / sqrt(9.0 * d);
+    double v = 1.0 + c * x;
+    bool ok = false;
+    double r = 0.0;
+    if (v > 0.0) {
+      v = v * v * v;
+      const double x2 = x * x;
+      if (u < 1.0 - 0.0331 * (x2 * x2)) ok = true;
+      else if (mmb_log(u) < 0.5 * x2 + d * (1.0 - v + mmb_log(v))) ok = true;
+      r = d * v;
+    }
+    if (!ok) {
+      uint32_t kn = 0, ku = 0;
+      r = mmb_gamma_mt(a, &rn, &ru, &kn, &ku);
+    }
+    return r;
+  }
+  // value of lane b (group-relative, wave-uniform b) of each 32-lane group
+  __device__ __forceinline__ static double lane_value(double v, int b) {
+    const uint64_t u = mmb_d2u(v);
+    const int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+    const uint32_t lo0 = (uint32_t)__builtin_amdgcn_readlane(lo, b), hi0 = (uint32_t)__builtin_amdgcn_readlane(hi, b);
+    const uint32_t lo1 = (uint32_t)__builtin_amdgcn_readlane(lo, b + 32), hi1 = (uint32_t)__builtin_amdgcn_readlane(hi, b + 32);
+    const bool up = (threadIdx.x & 32) != 0;
+    return mmb_u2d((uint64_t)(up ? lo1 : lo0) | ((uint64_t)(up ? hi1 : hi0) << 32));
+  }
+
   // ---------------------------------------------------------------- AMWG
   // amwg.jl:68-115 (sample!, setadapt!, amwg_sub!).
   __device__ __forceinline__ static void amwg(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,
@@ -408,7 +463,7 @@ struct Smp {
   // amm.jl:181-223.  LDS per chain: mat[TP] | z2[DP] | vv[DP] | mv[DP] | ia[2*DP ints]
   __device__ __forceinline__ static void amm(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,
                              const mmb_rng& ru, bool adapt, St& s, const Lc& l, const Grp<G>& g,
-                             double* lds) {
+                             double* lds, double upre) {
     const int d = B.d;
     const int T = mmb_tri(d);
     double* mat = lds;
@@ -517,7 +572,8 @@ struct Smp {
     const typename M::Prep pc = M::prep(B, s);
     double lx = M::logf_p(A, B, pc, s, l, g, x);
     double lv = M::logf_p(A, B, pc, s, l, g, v);
-    if (mmb_uniform(&ru, 0u) < mmb_exp(lx - lv)) {
+    const double ua = G == 32 ? upre : mmb_uniform(&ru, 0u);  // predraw() for 32-lane groups
+    if (ua < mmb_exp(lx - lv)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) v[r] = x[r];
     }

@@ -55,6 +55,10 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
 #ifdef MMB_PHASE_PROF
     const uint64_t _it0 = __builtin_amdgcn_s_memtime();
 #endif
+    // state-independent draws of the whole iteration, one block per lane (32-lane groups)
+    double pre = 0.0;
+    if constexpr (G == 32 && (KINDS & ((1u << MMB_SAMPLER_GIBBS) | (1u << MMB_SAMPLER_AMM))) != 0u)
+      pre = S::predraw(A, chain, it, g);
     for (int b = 0; b < A.nb; ++b) {
       // descriptor read through the constant address space: uniform scalar loads (s_load,
       // scalar cache) instead of vector loads that wait on the vector memory path
@@ -68,7 +72,8 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
           if constexpr ((KINDS >> MMB_SAMPLER_AMWG) & 1u) S::amwg(A, B, c, rn, ru, adapt, s, l, g);
           break;
         case MMB_SAMPLER_AMM:
-          if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) S::amm(A, B, c, rn, ru, adapt, s, l, g, lds);
+          if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) S::amm(A, B, c, rn, ru, adapt, s, l, g, lds,
+                                                                        G == 32 ? S::lane_value(pre, b) : 0.0);
           break;
         case MMB_SAMPLER_SLICE:
           if constexpr ((KINDS >> MMB_SAMPLER_SLICE) & 1u) {
@@ -89,7 +94,7 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
           const mmb_rng gn = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_N);
           const mmb_rng gu = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_GAMMA_U);
           MMB_PROF_START
-          M::gibbs(A, B, s, l, g, &rn, &gn, &gu);
+          M::gibbs(A, B, s, l, g, &rn, &gn, &gu, G == 32 ? S::lane_value(pre, b) : 0.0);
           MMB_PROF_MARK(7, g.lane)
         }
           break;
