@@ -389,8 +389,11 @@ struct Smp {
         const double ajj = sqrt(dl);
         const double rinv = 1.0 / ajj;
         // key: high word of a positive candidate, INT_MAX for a NaN candidate, else -1
+        // (three independent selects: no branchy nest for the compiler to serialise)
         const int hiw = (int)(mmb_d2u(dl) >> 32);
-        const int key = done ? -1 : (isnan(dl) ? 0x7fffffff : (dl > 0.0 ? hiw : -1));
+        int key = dl > 0.0 ? hiw : -1;
+        key = isnan(dl) ? 0x7fffffff : key;
+        key = done ? -1 : key;
         const int m = gmax_i32(key);
         const uint32_t win = (uint32_t)(__ballot(key == m) >> (threadIdx.x & 32));
         int p = __builtin_ctz(win | 0x80000000u);
@@ -404,7 +407,7 @@ struct Smp {
           rank = j;
           live = false;
         } else {
-          if (lane == 0) pks[j] = p;
+          pks[j] = p;  // same value from every lane of the group: no exec-mask change
           const bool piv = lane == p;
           if (piv) {
 #pragma unroll
