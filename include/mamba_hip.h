@@ -159,6 +159,28 @@ int mmb_gr_range(mmb_engine* e, double* minmax /* 2*p */);
 int64_t mmb_gr_len(const mmb_engine* e);
 int mmb_gr_partials(mmb_engine* e, const int32_t* link_kind, const double* shift, double* out);
 
+/* Posterior summaries of the device-kept draws, pooled over chains.
+ * mmb_chain_summary replaces the per-element work of summarystats(c; etype=:bm)
+ * (/root/reference/src/output/stats.jl:85-94) and mcse_bm (src/output/mcse.jl:10-19):
+ * per local chain k and monitored param j, out[(k*p + j)*MMB_SUMMARY_FIELDS + f] =
+ *   [sum x', sum x'^2, sum d_b, sum d_b^2, #full batches, head sum, head count,
+ *    tail sum, tail count, 0]    with x' = x - shift[j],
+ * where batches are runs of `batch_size` consecutive elements of vec(x) (chains
+ * concatenated; local chain k sits at position chain_base + k: the global chain id for a
+ * pooled multi-GPU summary, k for this engine alone), d_b = batch mean - shift[j] for the batches lying
+ * wholly in the chain, and head/tail are the chain's pieces of batches shared with the
+ * previous/next chain (joined by the host, across GPUs too).
+ * mmb_order_hist: one radix-select pass for quantile(c) (stats.jl:73-80): for each of
+ * `ntargets` key prefixes (order-preserving uint64 key of the double, bits above digit
+ * 56-8*pass), counts[t*256 + d] = #draws of `param` whose key matches prefix t and whose
+ * digit is d. */
+#define MMB_SUMMARY_FIELDS 10
+#define MMB_ORDER_MAX_TARGETS 16
+int mmb_chain_summary(mmb_engine* e, const double* shift /* p */, int64_t batch_size, int64_t chain_base,
+                      double* out /* K x p x MMB_SUMMARY_FIELDS */);
+int mmb_order_hist(mmb_engine* e, int param, int ntargets, const uint64_t* prefix, int pass,
+                   uint64_t* counts /* ntargets x 256 */);
+
 /* Timing / sync (bench.py roofline) */
 int mmb_sync(mmb_engine* e);
 int mmb_kernel_time(const mmb_engine* e, double* total_ms, int64_t* launches, int64_t* units);

@@ -14,6 +14,7 @@ MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = 1, 2, 3
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
 MMB_ABI_VERSION = 2
+MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
 MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
 MMB_LINE_BETA, MMB_LINE_S2 = 0, 1
@@ -74,6 +75,8 @@ def _declare(lib):
         "mmb_gr_range": (C.c_int, [P, D]),
         "mmb_gr_len": (I64, [P]),
         "mmb_gr_partials": (C.c_int, [P, C.POINTER(I32), D, D]),
+        "mmb_chain_summary": (C.c_int, [P, D, I64, I64, D]),
+        "mmb_order_hist": (C.c_int, [P, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_int, C.POINTER(C.c_uint64)]),
         "mmb_sync": (C.c_int, [P]),
         "mmb_kernel_time": (C.c_int, [P, D, C.POINTER(I64), C.POINTER(I64)]),
         "mmb_state_bytes": (C.c_int, [P, D]),

@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "lib", "libmambahip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-SOURCES = ["sweep.hip", "gr.hip", "logistic.hip", "engine.cpp"]
+SOURCES = ["sweep.hip", "gr.hip", "logistic.hip", "summary.hip", "engine.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
 

@@ -24,6 +24,10 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
                                hipStream_t st);
+hipError_t mmb_launch_chain_summary(int P, int64_t n, int K, int64_t kg0, int64_t bs, const double* draws,
+                                    const double* shift, double* out, hipStream_t st);
+hipError_t mmb_launch_order_hist(int P, int j, int64_t n, int K, const double* draws, int nt,
+                                 const uint64_t* prefix, int pass, unsigned long long* counts, hipStream_t st);
 hipError_t mmb_launch_gr_stats(int pmon, int64_t n, int K, const double* draws, const int32_t* link,
                                const double* shift, double* stats, hipStream_t st);
 
@@ -1009,6 +1013,53 @@ int mmb_gr_partials(mmb_engine* e, const int32_t* link, const double* shift, dou
   (void)hipFree(dl);
   (void)hipFree(ds);
   (void)hipFree(dout);
+  return 0;
+}
+
+// ---------------------------------------------------------------- posterior summaries
+int mmb_chain_summary(mmb_engine* e, const double* shift, int64_t batch_size, int64_t chain_base, double* out) {
+  if (!e || !shift || !out) return fail(e, MMB_E_ARG, "null argument");
+  if (batch_size < 1) return fail(e, MMB_E_ARG, "batch size must be positive");
+  if (chain_base < 0) return fail(e, MMB_E_ARG, "chain_base must be >= 0");
+  if (e->n_kept < 1) return fail(e, MMB_E_STATE, "no device-kept draws (run with keep_device=1)");
+  HIPCHK(e, hipSetDevice(e->device));
+  const int p = e->pmon;
+  const size_t nout = (size_t)e->K * p * MMB_SUMMARY_FIELDS;
+  double *ds = nullptr, *dout = nullptr;
+  HIPCHK(e, hipMalloc(&ds, p * sizeof(double)));
+  HIPCHK(e, hipMalloc(&dout, nout * sizeof(double)));
+  HIPCHK(e, hipMemcpyAsync(ds, shift, p * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  hipError_t st = mmb_launch_chain_summary(p, e->n_kept, (int)e->K, chain_base, batch_size, e->d_draws, ds,
+                                           dout, e->stream);
+  if (st == hipSuccess) st = hipMemcpyAsync(out, dout, nout * sizeof(double), hipMemcpyDeviceToHost, e->stream);
+  if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+  (void)hipFree(ds);
+  (void)hipFree(dout);
+  if (st != hipSuccess) return fail(e, MMB_E_HIP, "chain_summary: %s", hipGetErrorString(st));
+  return 0;
+}
+
+int mmb_order_hist(mmb_engine* e, int param, int ntargets, const uint64_t* prefix, int pass, uint64_t* counts) {
+  if (!e || !prefix || !counts) return fail(e, MMB_E_ARG, "null argument");
+  if (param < 0 || param >= e->pmon) return fail(e, MMB_E_ARG, "param %d out of range", param);
+  if (ntargets < 1 || ntargets > MMB_ORDER_MAX_TARGETS) return fail(e, MMB_E_ARG, "1 <= ntargets <= %d",
+                                                                      MMB_ORDER_MAX_TARGETS);
+  if (pass < 0 || pass > 7) return fail(e, MMB_E_ARG, "pass must be 0..7");
+  if (e->n_kept < 1) return fail(e, MMB_E_STATE, "no device-kept draws (run with keep_device=1)");
+  HIPCHK(e, hipSetDevice(e->device));
+  uint64_t* dp = nullptr;
+  unsigned long long* dc = nullptr;
+  HIPCHK(e, hipMalloc(&dp, ntargets * sizeof(uint64_t)));
+  HIPCHK(e, hipMalloc(&dc, (size_t)ntargets * 256 * sizeof(unsigned long long)));
+  hipError_t st = hipMemcpyAsync(dp, prefix, ntargets * sizeof(uint64_t), hipMemcpyHostToDevice, e->stream);
+  if (st == hipSuccess)
+    st = mmb_launch_order_hist(e->pmon, param, e->n_kept, (int)e->K, e->d_draws, ntargets, dp, pass, dc, e->stream);
+  if (st == hipSuccess)
+    st = hipMemcpyAsync(counts, dc, (size_t)ntargets * 256 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream);
+  if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+  (void)hipFree(dp);
+  (void)hipFree(dc);
+  if (st != hipSuccess) return fail(e, MMB_E_HIP, "order_hist: %s", hipGetErrorString(st));
   return 0;
 }
 

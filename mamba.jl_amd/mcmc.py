@@ -50,6 +50,7 @@ class Engine:
     def init_chains(self, init, chain_offset=0, seed=1):
         init = np.ascontiguousarray(init, dtype=np.float64)
         self.K = init.shape[0]
+        self.chain_offset = int(chain_offset)
         self._chk(self.lib.mmb_init_chains(self.h, abi.dptr(init), self.K, int(chain_offset),
                                            C.c_uint64(int(seed))))
 
@@ -139,6 +140,22 @@ class Engine:
                                            abi.dptr(shift), abi.dptr(out)))
         return out
 
+    # posterior-summary partials of the device-kept draws (summary.py pools them)
+    def chain_summary(self, shift, batch_size=100, chain_base=0):
+        shift = np.ascontiguousarray(shift, dtype=np.float64)
+        out = np.empty((self.K, self.pmon, abi.MMB_SUMMARY_FIELDS))
+        self._chk(self.lib.mmb_chain_summary(self.h, abi.dptr(shift), int(batch_size), int(chain_base),
+                                             abi.dptr(out)))
+        return out
+
+    def order_hist(self, param, prefixes, npass):
+        pre = np.ascontiguousarray(prefixes, dtype=np.uint64)
+        out = np.empty((pre.size, 256), dtype=np.uint64)
+        u64 = C.POINTER(C.c_uint64)
+        self._chk(self.lib.mmb_order_hist(self.h, int(param), int(pre.size), pre.ctypes.data_as(u64), int(npass),
+                                          out.ctypes.data_as(u64)))
+        return out
+
 
 class Chains:
     """Chains / ModelChains (src/output/chains.jl:5-11, modelchains.jl): value is
@@ -160,9 +177,30 @@ class Chains:
     def __getitem__(self, name):
         return self.value[:, self.names.index(name), :]
 
-    def describe(self):
-        v = self.value
-        return {nm: {"mean": float(v[:, j, :].mean()), "sd": float(v[:, j, :].std(ddof=1))}
+    def _device_engine(self):
+        eng = self.engine
+        if eng is None or eng.h is None or eng.num_kept() != self.value.shape[0] or self.value.shape[0] == 0:
+            raise ArgumentError("summaries run on the device-kept draws: sample with keep_device=True "
+                                "(the engine holds the last window's draws)")
+        return eng
+
+    def summarystats(self, batch_size=100):
+        """summarystats(c; etype=:bm) (stats.jl:85-94): p x [Mean, SD, Naive SE, MCSE, ESS]."""
+        from .summary import summarystats_sharded
+        return summarystats_sharded(self._device_engine(), batch_size)
+
+    def quantile(self, q=(0.025, 0.25, 0.5, 0.75, 0.975)):
+        """quantile(c; q) (stats.jl:73-80), pooled over iterations and chains: p x len(q)."""
+        from .summary import quantile_sharded
+        return quantile_sharded(self._device_engine(), q)
+
+    def describe(self, q=(0.025, 0.25, 0.5, 0.75, 0.975), batch_size=100):
+        """describe(c) (stats.jl:42-52): summarystats and quantiles per monitored name."""
+        ss = self.summarystats(batch_size)
+        qs = self.quantile(q)
+        labels = ["Mean", "SD", "Naive SE", "MCSE", "ESS"]
+        return {nm: {**{lb: float(ss[j, i]) for i, lb in enumerate(labels)},
+                     **{f"{100 * x}%": float(qs[j, t]) for t, x in enumerate(q)}}
                 for j, nm in enumerate(self.names)}
 
 

@@ -196,3 +196,46 @@ def test_logistic_device_gelman_rubin_matches_host(mamba):
         ps_host, mp_host = mamba.gelmandiag(d, transform=transform, mpsrf=True)
         np.testing.assert_allclose(ps_dev, ps_host, rtol=1e-8)
         assert mp_dev == pytest.approx(mp_host, rel=1e-6)
+
+
+def _summary_ref():
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import summary_ref
+    return summary_ref
+
+
+@pytest.mark.parametrize("iters,burnin,thin,bs,K", [(400, 100, 2, 100, 1024), (375, 0, 1, 100, 300),
+                                                     (60, 10, 1, 128, 257)])
+def test_device_summarystats_and_quantiles(mamba, iters, burnin, thin, bs, K):
+    """summarystats (stats.jl:85-94, mcse_bm mcse.jl:10-19) and quantile (stats.jl:73-80)
+    from the device-kept draws vs the oracle restatement on the same draws: sums within
+    rtol 1e-10 (reduction order differs), order statistics exact.  Covers batches that
+    straddle chains (n % bs != 0) and batches longer than a chain (bs > n)."""
+    sr = _summary_ref()
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(K, seed=5), seed=6)
+    d = eng.run(iters, burnin=burnin, thin=thin, keep_device=True)
+    sim = mamba.Chains(d, m.monitor_names, burnin + thin, thin, np.arange(1, K + 1), m, eng)
+    got = sim.summarystats(bs)
+    ref = sr.summarystats(d, bs)
+    np.testing.assert_allclose(got[:, :4], ref[:, :4], rtol=1e-10)
+    np.testing.assert_allclose(got[:, 4], ref[:, 4], rtol=1e-8)
+    q = (0.025, 0.25, 0.5, 0.75, 0.975)
+    np.testing.assert_array_equal(sim.quantile(q), sr.quantile(d, q))
+    desc = sim.describe()
+    assert set(desc) == {"s2_c", "mu_beta", "alpha0"} and desc["mu_beta"]["Mean"] == got[1, 0]
+
+
+def test_device_summary_logistic_many_params(mamba):
+    """p = 50 monitored values (one grid row per param)."""
+    sr = _summary_ref()
+    m, _ = logistic(mamba, 1000, 50)
+    eng = mamba.Engine(m)
+    eng.init_chains(np.random.default_rng(3).normal(0.0, 0.1, (40, 50)), seed=4)
+    d = eng.run(80, burnin=20, thin=1, model_burnin=20, keep_device=True)
+    got = mamba.summarystats_sharded(eng, batch_size=50)
+    np.testing.assert_allclose(got[:, :4], sr.summarystats(d, 50)[:, :4], rtol=1e-9)
+    np.testing.assert_array_equal(mamba.quantile_sharded(eng, (0.1, 0.5, 0.9)), sr.quantile(d, (0.1, 0.5, 0.9)))
