@@ -67,7 +67,7 @@ struct mmb_engine {
   DBlock* d_blocks = nullptr;
   // logistic (config 4): padded X/y and the NUTS machine state (logistic.h)
   int lg_N = 0, lg_p = 0, lg_rps = 0;
-  double *lg_X = nullptr, *lg_Xt = nullptr, *lg_y = nullptr;
+  double *lg_X = nullptr, *lg_y = nullptr;
   double *lg_vec = nullptr, *lg_sc = nullptr, *lg_frames = nullptr, *lg_pos = nullptr;
   double *lg_gpart = nullptr, *lg_lpart = nullptr;
   int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr;
@@ -352,7 +352,6 @@ void mmb_destroy(mmb_engine* e) {
   free_dev(e);
   if (e->d_data) (void)hipFree(e->d_data);
   if (e->lg_X) (void)hipFree(e->lg_X);
-  if (e->lg_Xt) (void)hipFree(e->lg_Xt);
   if (e->lg_y) (void)hipFree(e->lg_y);
   if (e->lg_hcount) (void)hipHostFree(e->lg_hcount);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
@@ -383,22 +382,19 @@ int mmb_set_data(mmb_engine* e, const char* name, const double* x, int64_t n) {
       return fail(e, MMB_E_ARG, "logistic: unknown input %s", name);
     }
     e->have_data = !e->X.empty() && !e->y.empty();
-    if (e->have_data) {  // padded device copies: X [Np][64], Xt [64][Np], y [Np]
+    if (e->have_data) {  // padded device copies: X [Np][64], y [Np]
       const size_t Np = (size_t)MMB_LG_NG * MMB_LG_NS * e->lg_rps;
-      std::vector<double> hx(Np * MMB_LG_DV, 0.0), hxt(Np * MMB_LG_DV, 0.0), hy(Np, 0.0);
+      std::vector<double> hx(Np * MMB_LG_DV, 0.0), hy(Np, 0.0);
       for (int i = 0; i < e->lg_N; ++i) {
         for (int k = 0; k < e->lg_p; ++k) {
           hx[(size_t)i * MMB_LG_DV + k] = e->X[(size_t)i * e->lg_p + k];
-          hxt[(size_t)k * Np + i] = e->X[(size_t)i * e->lg_p + k];
         }
         hy[i] = e->y[i];
       }
       HIPCHK(e, hipSetDevice(e->device));
       if (!e->lg_X) HIPCHK(e, hipMalloc(&e->lg_X, hx.size() * sizeof(double)));
-      if (!e->lg_Xt) HIPCHK(e, hipMalloc(&e->lg_Xt, hxt.size() * sizeof(double)));
       if (!e->lg_y) HIPCHK(e, hipMalloc(&e->lg_y, hy.size() * sizeof(double)));
       HIPCHK(e, hipMemcpy(e->lg_X, hx.data(), hx.size() * sizeof(double), hipMemcpyHostToDevice));
-      HIPCHK(e, hipMemcpy(e->lg_Xt, hxt.data(), hxt.size() * sizeof(double), hipMemcpyHostToDevice));
       HIPCHK(e, hipMemcpy(e->lg_y, hy.data(), hy.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     return 0;
@@ -669,7 +665,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.burnin = a->burnin; A.thin = a->thin; A.model_burnin = a->model_burnin; A.kept_origin = kept0;
   A.prior_sd = e->spec.prior_sd;
   A.target = h.spec.target;
-  A.X = e->lg_X; A.Xt = e->lg_Xt; A.y = e->lg_y;
+  A.X = e->lg_X; A.y = e->lg_y;
   A.vals = e->d_vals; A.vec = e->lg_vec; A.sc = e->lg_sc; A.iv = e->lg_iv; A.itc = e->lg_itc;
   A.kind = h.spec.sampler;
   A.frames = e->lg_frames; A.tm = h.m; A.tflags = h.flags;

@@ -25,7 +25,6 @@ struct LgArgs {
   int64_t burnin, thin, model_burnin, kept_origin;
   double prior_sd, target;
   const double* X;         // [Np][64] row-major, zero padded (rows and columns)
-  const double* Xt;        // [64][Np] transposed copy (A operand of X * B)
   const double* y;         // [N_pad]
   double* vals;            // [K][64] beta (the NUTS variate v)
   double* vec;             // [K][MMB_LG_NVEC][64]

@@ -201,97 +201,146 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
   }
 }
 
-// 1-D grid of 16 * ceil(K/16) workgroups of 4 waves.  Workgroup -> (group gi, chain tile):
-// blocks are dealt round-robin over the 8 XCDs, so XCD x gets groups 2x and 2x+1 only and its
-// L2 holds just those rows of X; tiles ascend with the block id, so the blocks beyond the
-// active count (the end of a window) are the last dispatched and exit at once.
-// Wave w computes sub-range 4*gi + w for the tile's 16 chains; the 4 sub-range partials are
-// combined through LDS in the spec order.  Lane l: chain column l & 15, k-group l >> 4.
+// 1-D grid of MMB_LG_NG * ceil(K/64) workgroups of 4 waves.  Workgroup -> (group gi, 64-chain
+// tile ct): blocks are dealt round-robin over the 8 XCDs, so XCD x gets groups 2x and 2x+1
+// only and its L2 holds just those rows of X; tiles ascend with the block id, so the blocks
+// beyond the active count (the end of a window) are the last dispatched and exit at once.
+// Wave w owns chains ct*64 + 16w .. +15 (lane l: chain column l & 15, k-group l >> 4) and
+// walks the group's MMB_LG_NS sub-ranges in order, folding their partials as ((P0+P1)+P2)+.. in
+// registers (the summation spec the oracle restates).  The workgroup stages each 32-row
+// pass of X once in LDS for all 4 waves (4x fewer L2 reads per MFMA than per-wave loads,
+// which were the bottleneck: a 16x16x4 f64 MFMA issues every 64 cycles per SIMD and needs
+// its 512-B A operand; measured tools/mfma_f64_probe.hip), prefetching the next pass into
+// registers while the current one is computed.
+// LDS row stride 66 doubles: the first GEMM's A reads (16 rows x 4 k-groups) hit 32
+// distinct bank pairs per half-wave; the second GEMM's reads are at most 2-way.
 #ifndef MMB_LG_WAVES
-#define MMB_LG_WAVES 3
+#define MMB_LG_WAVES 2
 #endif
+#define LG_RB 32   // rows per staged pass (two 16-row MFMA blocks)
+#define LG_LD 66   // padded LDS row stride (doubles)
+#define LG_PER (LG_RB * 64 / 256)  // doubles of a pass staged per thread
 __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs A, int parity) {
-  __shared__ double red[MMB_LG_NS][4][4][64];  // [wave][p-tile][reg][lane]
-  __shared__ double lred[MMB_LG_NS][16];
+  __shared__ __attribute__((aligned(16))) double xs[LG_RB][LG_LD];
+  __shared__ double ys[LG_RB];
   const int nact = A.count[parity];
   if (blockIdx.x == 0 && threadIdx.x == 0 && nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
   const int b = (int)blockIdx.x;
+  constexpr int GPX = MMB_LG_NG / 8;  // groups per XCD
   const int idx = b >> 3;
-  const int gi = 2 * (b & 7) + (idx & 1);
-  const int tile = idx >> 1;
-  if (tile * 16 >= nact) return;
-  const int w = (int)(threadIdx.x >> 6);
-  const int l = (int)(threadIdx.x & 63);
+  const int gi = GPX * (b & 7) + idx % GPX;
+  const int ct = idx / GPX;
+  if (ct * 64 >= nact) return;  // uniform over the workgroup
+  const int tid = (int)threadIdx.x;
+  const int w = tid >> 6;
+  const int l = tid & 63;
   const int lc = l & 15, lq = l >> 4;
-  const int slot = tile * 16 + lc;
+  const int slot = ct * 64 + w * 16 + lc;
   const bool live = slot < nact;
   double bpos[13];
 #pragma unroll
   for (int kk = 0; kk < 13; ++kk) bpos[kk] = live ? A.pos[(size_t)slot * 64 + 4 * kk + lq] : 0.0;
-  mmb_d4 acc[4];
+  mmb_d4 tot[4], acc[4];
+  double ltot = 0.0;
+  const int rps = A.rps;
+  const int npass = (rps + LG_RB - 1) / LG_RB;
+  // staging map: thread tid moves X[r0 + e*8 + (tid >> 3)... ] -- 8 consecutive doubles of one row
+  const int srow = tid >> 3, scol = (tid & 7) * 8;  // 32 rows x 8 segments of 8 doubles
+  double pf[LG_PER];
+  double pfy = 0.0;
+  auto fetch = [&](int r0, int nrows) {
+    const double* src = A.X + (size_t)(r0 + srow) * 64 + scol;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
-  double lsum = 0.0;
-  const int nb = A.rps / 16;
-  const int rbase = (gi * MMB_LG_NS + w) * A.rps;
-  // two 16-row blocks per pass: their X*B chains (13 dependent MFMAs each) interleave;
-  // the residual and X'*res steps then run block by block, so every sum keeps row order
-  for (int bk = 0; bk < nb; bk += 2) {
-    const bool two = bk + 1 < nb;
-    const int r0 = rbase + 16 * bk;
-    const double* xa = A.Xt + (size_t)lq * A.Np + r0 + lc;
-    mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
-    if (two) {
+    for (int e = 0; e < LG_PER; e += 2) {
+      const double2 v = srow < nrows ? *(const double2*)(src + e) : make_double2(0.0, 0.0);
+      pf[e] = v.x;
+      pf[e + 1] = v.y;
+    }
+    pfy = tid < nrows ? A.y[r0 + tid] : 0.0;
+  };
+  fetch((gi * MMB_LG_NS) * rps, rps < LG_RB ? rps : LG_RB);
+  for (int s = 0; s < MMB_LG_NS; ++s) {
+    const int rbase = (gi * MMB_LG_NS + s) * rps;
 #pragma unroll
-      for (int kk = 0; kk < 13; ++kk) {
-        eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np], bpos[kk], eta0, 0, 0, 0);
-        eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np + 16], bpos[kk], eta1, 0, 0, 0);
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
+    double lsum = 0.0;
+    for (int ps = 0; ps < npass; ++ps) {
+      const int r0 = rbase + ps * LG_RB;
+      const int nrows = rps - ps * LG_RB < LG_RB ? rps - ps * LG_RB : LG_RB;  // 16 or 32
+      __syncthreads();  // previous pass's LDS reads are done
+#pragma unroll
+      for (int e = 0; e < LG_PER; e += 2) *(double2*)&xs[srow][scol + e] = make_double2(pf[e], pf[e + 1]);
+      if (tid < LG_RB) ys[tid] = pfy;
+      __syncthreads();
+      {  // prefetch the next pass (or the next sub-range's first) while this one computes
+        int nr0 = r0 + LG_RB, nn = rps - (ps + 1) * LG_RB;
+        if (ps + 1 == npass) { nr0 = rbase + rps; nn = rps; }
+        if (nn > LG_RB) nn = LG_RB;
+        if (!(ps + 1 == npass && s + 1 == MMB_LG_NS)) fetch(nr0, nn);
       }
+      const bool two = nrows > 16;
+      mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
+      if (two) {
+#pragma unroll
+        for (int kk = 0; kk < 13; ++kk) {
+          eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
+          eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 + lc][4 * kk + lq], bpos[kk], eta1, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 13; ++kk)
+          eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
+      }
+      // residual terms of both blocks first (branch-free: padded rows have X = 0, eta = 0,
+      // and are masked by a select), so the scheduler can overlap block 1's VALU work with
+      // block 0's X'*res MFMAs; sums keep the row order of the spec
+      double sres[2][4], lps[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const mmb_d4 eta = h ? eta1 : eta0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = r0 + 16 * h + lq + 4 * i;
+          double lp, res;
+          mmb_logistic_terms(eta[i], ys[16 * h + lq + 4 * i], &lp, &res);
+          const bool in = row < A.N && (h == 0 || two);
+          lps[h][i] = in ? lp : 0.0;
+          sres[h][i] = in ? res : 0.0;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lsum = lsum + lps[h][i];
+        if (h == 1 && !two) break;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 * h + 4 * i + lq][16 * mt + lc], sres[h][i], acc[mt],
+                                                           0, 0, 0);
+      }
+    }
+    lsum = lsum + __shfl_xor(lsum, 16, 64);
+    lsum = lsum + __shfl_xor(lsum, 32, 64);
+    if (s == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) tot[mt] = acc[mt];
+      ltot = lsum;
     } else {
 #pragma unroll
-      for (int kk = 0; kk < 13; ++kk)
-        eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[(size_t)4 * kk * A.Np], bpos[kk], eta0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-      const int rb = r0 + 16 * h;
-      const mmb_d4 eta = h ? eta1 : eta0;
-      double s[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rb + lq + 4 * i;
-        double lp = 0.0, res = 0.0;
-        if (row < A.N) mmb_logistic_terms(eta[i], A.y[row], &lp, &res);
-        lsum = lsum + lp;
-        s[i] = res;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double* xt = A.X + (size_t)(rb + 4 * i + lq) * 64 + lc;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xt[16 * mt], s[i], acc[mt], 0, 0, 0);
-      }
+      for (int mt = 0; mt < 4; ++mt) tot[mt] = tot[mt] + acc[mt];
+      ltot = ltot + lsum;
     }
   }
-  lsum = lsum + __shfl_xor(lsum, 16, 64);
-  lsum = lsum + __shfl_xor(lsum, 32, 64);
+  if (!live) return;
+  // coefficient 16 mt + lq + 4 q of chain lc
+  double* gp = A.gpart + ((size_t)gi * A.K + slot) * 64;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) red[w][mt][q][l] = acc[mt][q];
-  if (l < 16) lred[w][l] = lsum;
-  __syncthreads();
-  if (!live) return;
-  // wave w writes p-tile w: coefficient 16w + lq + 4q of chain lc
-  double* gp = A.gpart + ((size_t)gi * A.K + slot) * 64;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const double v = ((red[0][w][q][l] + red[1][w][q][l]) + red[2][w][q][l]) + red[3][w][q][l];
-    gp[16 * w + lq + 4 * q] = v;
-  }
-  if (w == 0 && lq == 0)
-    A.lpart[(size_t)gi * A.K + slot] = ((lred[0][lc] + lred[1][lc]) + lred[2][lc]) + lred[3][lc];
+    for (int q = 0; q < 4; ++q) gp[16 * mt + lq + 4 * q] = tot[mt][q];
+  if (lq == 0) A.lpart[(size_t)gi * A.K + slot] = ltot;
 }
 
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st) {
@@ -305,6 +354,6 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t
   return hipGetLastError();
 }
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {
-  hipLaunchKernelGGL(lg_grad_kernel, dim3(16 * ((A.K + 15) / 16)), dim3(256), 0, st, A, parity);
+  hipLaunchKernelGGL(lg_grad_kernel, dim3(MMB_LG_NG * ((A.K + 63) / 64)), dim3(256), 0, st, A, parity);
   return hipGetLastError();
 }

@@ -300,17 +300,81 @@ MMB_HD double mmb_gamma_mt(double a, const mmb_rng* sn, const mmb_rng* su, uint3
  * (restated by the oracle): rows are split into MMB_LG_NG groups of MMB_LG_NS sub-ranges of
  * mmb_lg_rps(N) rows (a multiple of the 16-row MFMA tile).  Within a sub-range each
  * gradient component is one fma chain over its rows in order; a group's partial is
- * ((P0 + P1) + P2) + P3; the gradient is -beta/sd^2 + G0 + G1 + ... in group order. */
-#define MMB_LG_NG 16
-#define MMB_LG_NS 4
+ * ((P0 + P1) + P2) + ... over its MMB_LG_NS sub-ranges; the gradient is -beta/sd^2 + G0 + G1 + ... in group order. */
+#ifndef MMB_LG_NG
+#define MMB_LG_NG 32
+#endif
+#ifndef MMB_LG_NS
+#define MMB_LG_NS 2
+#endif
 #define MMB_LG_DV 64 /* coefficients per chain, padded (p <= 64) */
 MMB_HD int mmb_lg_rps(int N) {
   int per = (N + MMB_LG_NG * MMB_LG_NS - 1) / (MMB_LG_NG * MMB_LG_NS);
   return ((per + 15) / 16) * 16;
 }
+/* exp(x) for x <= 0, branch- and division-free (the logistic per-row terms run it for every
+ * row x chain of every gradient): k = round(x / ln2) by the 1.5*2^52 shift, two-step
+ * reduction by fma (|r| <= ln2/2), degree-13 Taylor polynomial in Horner form (truncation
+ * < 2^-57), 2^k through the exponent field (two steps below 2^-1021).  Only IEEE +, *, fma:
+ * bit-identical on host and device.  x < -745.2 -> 0; NaN -> NaN. */
+MMB_HD double mmb_exp_neg(double x) {
+  const double shift = 0x1.8p52, invln2 = 1.44269504088896338700e+00,
+               ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
+  const double xc = x > -745.2 ? x : -745.2;             /* NaN stays NaN through fma below */
+  const double kd = fma(xc, invln2, shift) - shift;
+  double r = fma(-kd, ln2HI, xc);
+  r = fma(-kd, ln2LO, r);
+  double p = 1.6059043836821613e-10;                  /* 1/13! */
+  p = fma(p, r, 2.08767569878681e-09);              /* 1/12! */
+  p = fma(p, r, 2.505210838544172e-08);
+  p = fma(p, r, 2.755731922398589e-07);
+  p = fma(p, r, 2.7557319223985893e-06);
+  p = fma(p, r, 2.48015873015873e-05);
+  p = fma(p, r, 1.984126984126984e-04);
+  p = fma(p, r, 1.388888888888889e-03);
+  p = fma(p, r, 8.333333333333333e-03);
+  p = fma(p, r, 4.1666666666666664e-02);
+  p = fma(p, r, 1.6666666666666666e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int64_t k = (int64_t)kd;                          /* -1075 .. 0 */
+  const double big = mmb_u2d(mmb_d2u(p) + ((uint64_t)k << 52));
+  const double small = mmb_u2d(mmb_d2u(p) + ((uint64_t)(k + 1000) << 52)) * 9.33263618503218878990e-302;
+  const double e = k >= -1021 ? big : small;
+  return x > -745.2 ? e : (x != x ? x : 0.0);
+}
+
+/* log1p(t) for t in [0, 1]: 2 atanh(s), s = t / (2 + t) <= 1/3, as the odd series
+ * 2 s sum_k s^(2k) / (2k + 1) to k = 16 (truncation < 2^-56); one division, no branches. */
+MMB_HD double mmb_log1p_unit(double t) {
+  const double s = t / (2.0 + t);
+  const double z = s * s;
+  double p = 1.0 / 33.0;
+  p = fma(p, z, 1.0 / 31.0);
+  p = fma(p, z, 1.0 / 29.0);
+  p = fma(p, z, 1.0 / 27.0);
+  p = fma(p, z, 1.0 / 25.0);
+  p = fma(p, z, 1.0 / 23.0);
+  p = fma(p, z, 1.0 / 21.0);
+  p = fma(p, z, 1.0 / 19.0);
+  p = fma(p, z, 1.0 / 17.0);
+  p = fma(p, z, 1.0 / 15.0);
+  p = fma(p, z, 1.0 / 13.0);
+  p = fma(p, z, 1.0 / 11.0);
+  p = fma(p, z, 1.0 / 9.0);
+  p = fma(p, z, 1.0 / 7.0);
+  p = fma(p, z, 1.0 / 5.0);
+  p = fma(p, z, 1.0 / 3.0);
+  const double s2 = 2.0 * s;
+  return fma(s2, z * p, s2);
+}
+
+/* Per observation of the logistic model: lp = y eta - softplus(eta), res = y - invlogit(eta),
+ * both from t = exp(-|eta|) (stable for any eta). */
 MMB_HD void mmb_logistic_terms(double eta, double y, double* lp, double* res) {
-  double t = mmb_exp(-fabs(eta));
-  double sp = (eta > 0.0 ? eta : 0.0) + mmb_log1p(t);
+  double t = mmb_exp_neg(-fabs(eta));
+  double sp = (eta > 0.0 ? eta : 0.0) + mmb_log1p_unit(t);
   *lp = y * eta - sp;
   double q = 1.0 / (1.0 + t);
   *res = y - (eta >= 0.0 ? q : t * q);

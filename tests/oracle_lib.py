@@ -37,7 +37,7 @@ class Oracle:
         L.orc_block_logpdf_grad.restype = C.c_double
         L.orc_block_logpdf_grad.argtypes = [P, DD, C.POINTER(I64), D, C.c_int, D, D]
         L.orc_pivoted_cholesky.argtypes = [C.c_int, D, D, C.POINTER(C.c_int)]
-        for f in ("orc_log", "orc_exp", "orc_log1p"):
+        for f in ("orc_log", "orc_exp", "orc_log1p", "orc_exp_neg", "orc_log1p_unit"):
             getattr(L, f).restype = C.c_double
             getattr(L, f).argtypes = [C.c_double]
         L.orc_sincos2pi.argtypes = [C.c_double, D, D]

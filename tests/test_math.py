@@ -32,6 +32,10 @@ def ulps(a, b):
     ("orc_exp", np.exp, lambda r: r.uniform(-740, 709, 20000)),
     ("orc_exp", np.exp, lambda r: r.uniform(-1, 1, 20000)),
     ("orc_log1p", np.log1p, lambda r: np.exp(r.uniform(-40, 3, 20000))),
+    ("orc_exp_neg", np.exp, lambda r: r.uniform(-745, 0, 20000)),
+    ("orc_exp_neg", np.exp, lambda r: -np.exp(r.uniform(-60, 0, 20000))),
+    ("orc_log1p_unit", np.log1p, lambda r: r.uniform(0, 1, 20000)),
+    ("orc_log1p_unit", np.log1p, lambda r: np.exp(r.uniform(-745, 0, 20000))),
 ])
 def test_elementary_within_one_ulp(oracle, fn, npf, gen):
     x = gen(np.random.default_rng(7))
@@ -39,7 +43,8 @@ def test_elementary_within_one_ulp(oracle, fn, npf, gen):
     got = np.array([f(float(v)) for v in x])
     ref = npf(x)
     bad = ulps(got, ref)
-    assert bad.max() <= (2 if fn == "orc_log1p" else 1), (x[bad.argmax()], got[bad.argmax()], ref[bad.argmax()])
+    tol = 2 if fn in ("orc_log1p", "orc_log1p_unit") else 1
+    assert bad.max() <= tol, (x[bad.argmax()], got[bad.argmax()], ref[bad.argmax()])
 
 
 def test_elementary_special_values(oracle):
@@ -48,6 +53,10 @@ def test_elementary_special_values(oracle):
     assert L.orc_log(1.0) == 0.0 and L.orc_exp(0.0) == 1.0
     assert L.orc_exp(800.0) == np.inf and L.orc_exp(-800.0) == 0.0 and L.orc_exp(-np.inf) == 0.0
     assert np.isnan(L.orc_exp(np.nan))
+    # logistic-term kernels (x <= 0, t in [0, 1])
+    assert L.orc_exp_neg(0.0) == 1.0 and L.orc_exp_neg(-800.0) == 0.0 and L.orc_exp_neg(-np.inf) == 0.0
+    assert np.isnan(L.orc_exp_neg(np.nan)) and L.orc_exp_neg(-745.1) == 5e-324
+    assert L.orc_log1p_unit(0.0) == 0.0 and L.orc_log1p_unit(1e-300) == 1e-300
     assert abs(L.orc_log(5e-324) - np.log(5e-324)) < 1e-12  # subnormal path
 
 
