@@ -15,6 +15,36 @@
 
 #define MMB_MAXB MMB_MAX_BLOCKS
 
+// Correctly rounded sqrt(x) and 1/y for operands well inside the normal range, without the
+// range handling of the generic sequences.  For x in [2^-700, 2^700] these are the very
+// instruction sequences the compiler emits for sqrt() / 1.0 / y (ocml: rsq + Goldschmidt +
+// two corrections; fdiv: rcp + two Newton steps + one correction) with the no-op parts
+// dropped: no 2^256 input scaling (x >= 2^-767), v_div_scale / v_div_fmas leave operands
+// unscaled (exponents within 768 of 1.0) and v_div_fixup passes finite non-zero quotients
+// through.  So they return the IEEE results bit for bit (the oracle uses C sqrt and /).
+// Callers check the range and take sqrt() / division otherwise.
+__device__ __forceinline__ bool mmb_fast_range(double x) { return x >= 0x1p-700 && x <= 0x1p700; }
+__device__ __forceinline__ double mmb_sqrt_inrange(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+}
+__device__ __forceinline__ double mmb_rcp_inrange(double y) {
+  double r = __builtin_amdgcn_rcp(y);
+  double e = fma(-y, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-y, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-y, r, 1.0);
+  return fma(e, r, r);
+}
+
 // Per-block descriptor passed in kernel arguments (constant memory, uniform access).
 struct DBlock {
   int32_t kind, nn, d, transform, form, adapt, batchsize, sigl_diag;

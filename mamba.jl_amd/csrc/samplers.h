@@ -361,9 +361,9 @@ struct Smp {
   }
 
   // pchol for 32-lane groups with one row per lane (rats), same results as pchol():
-  // * every lane computes sqrt / reciprocal of its own remaining diagonal while the pivot
-  //   is searched (the pivot lane's pair is exactly sqrt(val), 1/sqrt(val)); the pivot lane
-  //   publishes its reciprocal through LDS together with its factor row;
+  // * the pivot lane computes sqrt / reciprocal of its remaining diagonal by the in-range
+  //   sequences of device.h (bit-identical to sqrt() and 1.0 / x there) and publishes the
+  //   reciprocal through LDS together with its factor row;
   // * the search reduces the high words of the positive candidates as int32 (one DPP
   //   max per stage); a unique maximal high word is the unique maximum.  High-word ties
   //   and NaN candidates go to pivot_exact (dpstf2's first maximum in position order).
@@ -386,8 +386,6 @@ struct Smp {
     for (int j = 0; j < DMAX; ++j) {
       if (live && j < d) {
         const double dl = diag0 - work;
-        const double ajj = sqrt(dl);
-        const double rinv = 1.0 / ajj;
         // key: high word of a positive candidate, INT_MAX for a NaN candidate, else -1
         // (three independent selects: no branchy nest for the compiler to serialise)
         const int hiw = (int)(mmb_d2u(dl) >> 32);
@@ -409,10 +407,19 @@ struct Smp {
         } else {
           pks[j] = p;  // same value from every lane of the group: no exec-mask change
           const bool piv = lane == p;
+          double ajj = 0.0;
           if (piv) {
 #pragma unroll
             for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
             if (j & 1) prow[j - 1] = Lrow[j - 1];
+            double rinv;
+            if (mmb_fast_range(dl)) {  // the pivot's sqrt and reciprocal, IEEE results (device.h)
+              ajj = mmb_sqrt_inrange(dl);
+              rinv = mmb_rcp_inrange(ajj);
+            } else {
+              ajj = sqrt(dl);
+              rinv = 1.0 / ajj;
+            }
             prow[RI] = rinv;
           }
           grp_sync();
