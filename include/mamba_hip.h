@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 2
+#define MMB_ABI_VERSION 3
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -46,7 +46,8 @@ extern "C" {
 typedef enum {
   MMB_MODEL_LINE = 1,    /* doc/tutorial/line.jl:5-25   y ~ IsoNormal(xmat*beta, sqrt(s2)) */
   MMB_MODEL_RATS = 2,    /* doc/examples/rats.jl:48-97  hierarchical growth model */
-  MMB_MODEL_LOGISTIC = 3 /* build-defined:  y ~ Bernoulli(invlogit(X*beta)) */
+  MMB_MODEL_LOGISTIC = 3, /* build-defined:  y ~ Bernoulli(invlogit(X*beta)) */
+  MMB_MODEL_IR = 4        /* generic node IR: created by mmb_create_ir */
 } mmb_model_kind;
 
 /* node ids (Stochastic nodes that can appear in a sampling block) */
@@ -103,6 +104,81 @@ typedef struct {
   int32_t reserved[8];
 } mmb_model_spec;
 
+/* ---- generic node IR (ABI version 3) ----------------------------------
+ * A Mamba Model DAG (src/model/model.jl:5-27, src/model/dependent.jl:75-152) lowered by the
+ * host (mamba.jl_amd/ir.py; a Julia shim would walk m.nodes the same way):
+ *   - Logical nodes are inlined into the expressions of their Stochastic children;
+ *   - Stochastic nodes that no sampling block updates are fixed: values in the data pool;
+ *   - the sampled ones own slots [off, off+len) of the chain state (P = nvalues);
+ *   - each node's distribution parameters are stack-code expressions evaluated per element i
+ *     of the node (elementwise broadcast, src/distributions/distributionstruct.jl:142-158).
+ * Block ids in mmb_block_spec.nodes index `nodes`. */
+typedef enum {
+  MMB_IR_NORMAL = 1,      /* Normal(mu, sigma)                          RealDistribution      */
+  MMB_IR_ISONORMAL = 2,   /* MvNormal(mu[], sigma) (PDMats ScalMat)     node-level density    */
+  MMB_IR_INVGAMMA = 3,    /* InverseGamma(shape, scale)                 PositiveDistribution  */
+  MMB_IR_GAMMA = 4,       /* Gamma(shape, scale)                        PositiveDistribution  */
+  MMB_IR_EXPONENTIAL = 5, /* Exponential(scale)                         PositiveDistribution  */
+  MMB_IR_UNIFORM = 6,     /* Uniform(a, b), constant bounds lo/hi       bounded (affine logit) */
+  MMB_IR_BETA = 7,        /* Beta(a, b)                                 UnitDistribution      */
+  MMB_IR_BINOMIAL = 8,    /* Binomial(n, p)     fixed (observed) nodes only */
+  MMB_IR_POISSON = 9,     /* Poisson(lambda)    fixed (observed) nodes only */
+  MMB_IR_BERNOULLI = 10,  /* Bernoulli(p)       fixed (observed) nodes only */
+  MMB_IR_LOGICAL = 11     /* Logical: expr[0] is the value (monitored logicals) */
+} mmb_ir_family;
+
+/* expression code: one int32 word per op, op << 24 | arg; a push spills the previous top */
+enum {
+  MMB_IR_OP_END = 0,
+  MMB_IR_OP_CONST = 1,  /* push consts[arg] */
+  MMB_IR_OP_VAL = 2,    /* push state[arg] */
+  MMB_IR_OP_VALI = 3,   /* push state[arg + i] */
+  MMB_IR_OP_VALG = 4,   /* push state[arg + (int)pool[w + i]], w = the next code word */
+  MMB_IR_OP_DATA = 5,   /* push pool[arg + i] */
+  MMB_IR_OP_DATAS = 6,  /* push pool[arg] */
+  MMB_IR_OP_ADD = 16, MMB_IR_OP_SUB = 17, MMB_IR_OP_MUL = 18, MMB_IR_OP_DIV = 19,
+  MMB_IR_OP_NEG = 32, MMB_IR_OP_EXP = 33, MMB_IR_OP_LOG = 34, MMB_IR_OP_SQRT = 35,
+  MMB_IR_OP_INVLOGIT = 36, MMB_IR_OP_LOGIT = 37, MMB_IR_OP_ABS = 38
+};
+#define MMB_IR_MAX_STACK 16
+#define MMB_IR_MAX_TERMS 16
+#define MMB_IR_MAX_VALUES 512
+
+typedef struct {
+  int32_t family;    /* mmb_ir_family */
+  int32_t fixed;     /* 1: values in the pool at `off` (not sampled) */
+  int32_t off, len;  /* state slots (or pool offset) */
+  int32_t expr[3];   /* code offsets of the distribution parameters (Distributions order), -1 none */
+  int32_t cterm;     /* pool offset of a per-element constant (log binomial coefficient,
+                        -lgamma(k+1)) or -1 */
+  double lo, hi;     /* Uniform bounds */
+} mmb_ir_node;
+
+/* logpdf!(m, x, block, transform) terms (simulation.jl:77-90): params \ targets in block
+ * order, then targets in topological order; trans = node is a block param (evaluated with
+ * the block's transform) */
+typedef struct {
+  int32_t nterms;
+  int32_t term[MMB_IR_MAX_TERMS];
+  int32_t trans[MMB_IR_MAX_TERMS];
+} mmb_ir_block;
+
+typedef struct {
+  int32_t nvalues;              /* P */
+  int32_t nnodes;
+  const mmb_ir_node* nodes;
+  int32_t ncode;
+  const int32_t* code;
+  int32_t nconst;
+  const double* consts;
+  int64_t npool;
+  const double* pool;           /* data, fixed node values, gather indices (0-based), cterms */
+  int32_t nmon;
+  const int32_t* mon;           /* monitored node ids in Chains order, each contributing len values */
+  int32_t stack;                /* max expression stack depth (<= MMB_IR_MAX_STACK) */
+  mmb_ir_block blocks[MMB_MAX_BLOCKS];  /* one per sampling block of the spec */
+} mmb_ir_model;
+
 /* Arguments of one mcmc window (mcmc.jl:36-83). */
 typedef struct {
   int64_t iters;        /* window = iter+1 : iter+iters  (mcmc_master! `window`) */
@@ -119,6 +195,10 @@ typedef struct mmb_engine mmb_engine;
 /* Engine lifetime ---------------------------------------------------------------- */
 int mmb_abi_version(void);
 int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out);
+/* Node-IR model (spec->model == MMB_MODEL_IR): the IR is copied and validated (every code
+ * word, slot and pool range against the node lengths) before anything touches the device.
+ * Replaces the same fan-out as mmb_create for any Model lowered to the IR. */
+int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out);
 void mmb_destroy(mmb_engine* e);
 const char* mmb_last_error(const mmb_engine* e); /* e may be NULL: last global error */
 

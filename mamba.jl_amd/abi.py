@@ -10,10 +10,10 @@ import os
 MMB_MAX_BLOCKS = 8
 MMB_MAX_NODES_PER_BLOCK = 4
 
-MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = 1, 2, 3
+MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC, MMB_MODEL_IR = 1, 2, 3, 4
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
-MMB_ABI_VERSION = 2
+MMB_ABI_VERSION = 3
 MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
 MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
@@ -21,6 +21,14 @@ MMB_LINE_BETA, MMB_LINE_S2 = 0, 1
 (MMB_RATS_S2_C, MMB_RATS_ALPHA, MMB_RATS_MU_ALPHA, MMB_RATS_S2_ALPHA, MMB_RATS_BETA, MMB_RATS_MU_BETA,
  MMB_RATS_S2_BETA) = range(7)
 MMB_LOGISTIC_BETA = 0
+
+# node IR (include/mamba_hip.h)
+(MMB_IR_NORMAL, MMB_IR_ISONORMAL, MMB_IR_INVGAMMA, MMB_IR_GAMMA, MMB_IR_EXPONENTIAL, MMB_IR_UNIFORM, MMB_IR_BETA,
+ MMB_IR_BINOMIAL, MMB_IR_POISSON, MMB_IR_BERNOULLI, MMB_IR_LOGICAL) = range(1, 12)
+IR_OP = {"end": 0, "const": 1, "val": 2, "vali": 3, "valg": 4, "data": 5, "datas": 6,
+         "+": 16, "-": 17, "*": 18, "/": 19,
+         "neg": 32, "exp": 33, "log": 34, "sqrt": 35, "invlogit": 36, "logit": 37, "abs": 38}
+MMB_IR_MAX_STACK, MMB_IR_MAX_TERMS, MMB_IR_MAX_VALUES = 16, 16, 512
 
 ERRORS = {-1: "invalid argument", -2: "unsupported model/scheme", -3: "HIP runtime error",
           -4: "call out of order", -5: "out of memory"}
@@ -41,6 +49,24 @@ class ModelSpec(C.Structure):
                 ("prior_sd", C.c_double), ("reserved", C.c_int32 * 8)]
 
 
+class IrNode(C.Structure):
+    _fields_ = [("family", C.c_int32), ("fixed", C.c_int32), ("off", C.c_int32), ("len", C.c_int32),
+                ("expr", C.c_int32 * 3), ("cterm", C.c_int32), ("lo", C.c_double), ("hi", C.c_double)]
+
+
+class IrBlock(C.Structure):
+    _fields_ = [("nterms", C.c_int32), ("term", C.c_int32 * MMB_IR_MAX_TERMS),
+                ("trans", C.c_int32 * MMB_IR_MAX_TERMS)]
+
+
+class IrModel(C.Structure):
+    _fields_ = [("nvalues", C.c_int32), ("nnodes", C.c_int32), ("nodes", C.POINTER(IrNode)),
+                ("ncode", C.c_int32), ("code", C.POINTER(C.c_int32)), ("nconst", C.c_int32),
+                ("consts", C.POINTER(C.c_double)), ("npool", C.c_int64), ("pool", C.POINTER(C.c_double)),
+                ("nmon", C.c_int32), ("mon", C.POINTER(C.c_int32)), ("stack", C.c_int32),
+                ("blocks", IrBlock * MMB_MAX_BLOCKS)]
+
+
 class RunArgs(C.Structure):
     _fields_ = [("iters", C.c_int64), ("burnin", C.c_int64), ("thin", C.c_int64),
                 ("model_burnin", C.c_int64), ("draws", C.POINTER(C.c_double)),
@@ -57,6 +83,7 @@ def _declare(lib):
     sig = {
         "mmb_abi_version": (C.c_int, []),
         "mmb_create": (C.c_int, [C.POINTER(ModelSpec), C.c_int, C.POINTER(C.c_void_p)]),
+        "mmb_create_ir": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_int, C.POINTER(C.c_void_p)]),
         "mmb_destroy": (None, [P]),
         "mmb_last_error": (C.c_char_p, [P]),
         "mmb_set_data": (C.c_int, [P, C.c_char_p, D, I64]),

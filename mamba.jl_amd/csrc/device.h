@@ -12,6 +12,7 @@
 
 #include "../../include/mamba_hip.h"
 #include "mmb_math.h"
+#include "ir_math.h"
 
 #define MMB_MAXB MMB_MAX_BLOCKS
 
@@ -66,6 +67,7 @@ struct DBlock {
   double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
   double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
   double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)
+  int32_t ir_blk;        // node IR: index into SweepArgs::ir_blocks
 };
 
 struct SweepArgs {
@@ -86,6 +88,17 @@ struct SweepArgs {
   double xm[5];          // rats: x - xbar
   double lx[5], ly[5];   // line data
   const DBlock* blocks;  // device array [nb] (uniform, scalar-cache loads)
+  // node IR (MMB_MODEL_IR, ir.h): tables, state row length, LDS layout per chain
+  const mmb_ir_node* ir_nodes;
+  const int32_t* ir_code;
+  const double* ir_const;
+  const double* ir_pool;
+  const mmb_ir_block* ir_blocks;
+  const int32_t* ir_mon;
+  int32_t ir_nmon, ir_pmon;
+  int32_t ir_vs;         // doubles per chain row of `vals` (P rounded up to 32)
+  int32_t ir_amm;        // AMM scratch doubles at the start of a chain's LDS (0 without AMM)
+  int32_t ir_lds;        // LDS doubles per chain
 };
 
 // Block descriptors are read-only for a launch: read them through the constant address

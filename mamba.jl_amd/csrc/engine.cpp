@@ -12,12 +12,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "device.h"
 #include "models.h"
 #include "nuts.h"
 #include "logistic.h"
+#include "ir.h"
 
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st);
@@ -78,6 +80,16 @@ struct mmb_engine {
   double* d_draws = nullptr;
   size_t draws_cap = 0;
   int64_t n_kept = 0;
+  // node IR (MMB_MODEL_IR): host copies of the lowered model, device tables
+  std::vector<mmb_ir_node> ir_nodes;
+  std::vector<int32_t> ir_code, ir_mon;
+  std::vector<double> ir_const, ir_pool;
+  std::vector<mmb_ir_block> ir_blocks;
+  int ir_stack = 0;
+  mmb_ir_node* d_ir_nodes = nullptr;
+  int32_t *d_ir_code = nullptr, *d_ir_mon = nullptr;
+  double *d_ir_const = nullptr, *d_ir_pool = nullptr;
+  mmb_ir_block* d_ir_blocks = nullptr;
   // timing
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> evpool;  // 2 per launch when time_kernels
@@ -104,10 +116,17 @@ static int fail(mmb_engine* e, int code, const char* fmt, ...) {
       return fail((e), MMB_E_HIP, "%s failed: %s", #call, hipGetErrorString(_st));       \
   } while (0)
 
-static int node_dim(const mmb_model_spec& s, int node, bool* positive) {
+static int node_dim(const mmb_model_spec& s, const mmb_ir_model* ir, int node, bool* positive) {
   bool pos = false;
   int d = -1;
-  if (s.model == MMB_MODEL_LINE) {
+  if (s.model == MMB_MODEL_IR) {
+    // sampled nodes only: not fixed, not Logical, not a discrete family
+    if (ir && node >= 0 && node < ir->nnodes) {
+      const mmb_ir_node& n = ir->nodes[node];
+      const bool ok = !n.fixed && n.family >= MMB_IR_NORMAL && n.family <= MMB_IR_BETA;
+      d = ok ? n.len : -1;
+    }
+  } else if (s.model == MMB_MODEL_LINE) {
     if (node == MMB_LINE_BETA) d = 2;
     else if (node == MMB_LINE_S2) { d = 1; pos = true; }
   } else if (s.model == MMB_MODEL_RATS) {
@@ -160,7 +179,7 @@ const char* mmb_last_error(const mmb_engine* e) {
   return g_last_error.c_str();
 }
 
-int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
+static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out) {
   if (!spec || !out) return fail(nullptr, MMB_E_ARG, "null argument");
   *out = nullptr;
   if (spec->nblocks < 1 || spec->nblocks > MMB_MAX_BLOCKS)
@@ -174,6 +193,24 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
   } else if (e->model == MMB_MODEL_LINE) {
     e->P = 3; e->pmon = 3; e->VS = Mdl<MMB_MODEL_LINE>::VS;
     e->DP = Mdl<MMB_MODEL_LINE>::DP; e->TP = Mdl<MMB_MODEL_LINE>::TP;
+  } else if (e->model == MMB_MODEL_IR) {
+    if (!ir) {
+      delete e;
+      return fail(nullptr, MMB_E_ARG, "node-IR models are created with mmb_create_ir");
+    }
+    e->P = ir->nvalues;
+    e->pmon = 0;
+    for (int q = 0; q < ir->nmon; ++q) e->pmon += ir->nodes[ir->mon[q]].len;
+    e->VS = (ir->nvalues + 31) / 32 * 32;
+    e->DP = Mdl<MMB_MODEL_IR>::DP; e->TP = Mdl<MMB_MODEL_IR>::TP;
+    e->ir_nodes.assign(ir->nodes, ir->nodes + ir->nnodes);
+    e->ir_code.assign(ir->code, ir->code + ir->ncode);
+    e->ir_const.assign(ir->consts, ir->consts + ir->nconst);
+    e->ir_pool.assign(ir->pool, ir->pool + ir->npool);
+    e->ir_mon.assign(ir->mon, ir->mon + ir->nmon);
+    e->ir_blocks.assign(ir->blocks, ir->blocks + spec->nblocks);
+    e->ir_stack = ir->stack;
+    e->have_data = true;  // the pool carries the data
   } else if (e->model == MMB_MODEL_LOGISTIC) {
     if (spec->ncoef < 1 || spec->ncoef > MMB_LG_DV || spec->nobs < 1 || !(spec->prior_sd > 0.0)) {
       delete e;
@@ -206,7 +243,7 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
           delete e;
           return fail(nullptr, MMB_E_ARG, "block %d: repeated node", b);
         }
-      int nd = node_dim(*spec, s.nodes[a], nullptr);
+      int nd = node_dim(*spec, ir, s.nodes[a], nullptr);
       if (nd < 0) {
         delete e;
         return fail(nullptr, MMB_E_ARG, "block %d: node id %d invalid for model", b, s.nodes[a]);
@@ -220,6 +257,11 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
     }
     h.d = d;
     h.T = tri(d);
+    if (e->model == MMB_MODEL_IR && d > Mdl<MMB_MODEL_IR>::DMAX) {
+      delete e;
+      return fail(nullptr, MMB_E_UNSUPPORTED, "node IR: block %d has %d elements (max %d)", b, d,
+                  Mdl<MMB_MODEL_IR>::DMAX);
+    }
     if (e->model == MMB_MODEL_RATS && nvec > 0 && (s.nnodes != 1)) {
       delete e;
       return fail(nullptr, MMB_E_UNSUPPORTED, "rats: alpha/beta must form their own block");
@@ -256,6 +298,10 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
         }
         break;
       case MMB_SAMPLER_GIBBS:
+        if (e->model == MMB_MODEL_IR) {
+          delete e;
+          return fail(nullptr, MMB_E_UNSUPPORTED, "Gibbs (user Sampler closures) cannot be lowered to the node IR");
+        }
         if (s.nnodes != 1) {
           delete e;
           return fail(nullptr, MMB_E_UNSUPPORTED, "Gibbs: one node per block");
@@ -304,8 +350,127 @@ int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
     delete e;
     return fail(nullptr, MMB_E_HIP, "stream/event creation failed");
   }
+  if (e->model == MMB_MODEL_IR) {  // device copies of the IR tables (read-only for every launch)
+    bool ok = true;
+    auto up = [&](auto** dst, const auto& v) {
+      using T = typename std::remove_reference<decltype(v)>::type::value_type;
+      if (!ok) return;
+      ok = hipMalloc((void**)dst, std::max<size_t>(v.size(), 1) * sizeof(T)) == hipSuccess &&
+           (v.empty() || hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess);
+    };
+    up(&e->d_ir_nodes, e->ir_nodes);
+    up(&e->d_ir_code, e->ir_code);
+    up(&e->d_ir_const, e->ir_const);
+    up(&e->d_ir_pool, e->ir_pool);
+    up(&e->d_ir_mon, e->ir_mon);
+    up(&e->d_ir_blocks, e->ir_blocks);
+    if (!ok) {
+      mmb_destroy(e);
+      return fail(nullptr, MMB_E_HIP, "node IR upload failed");
+    }
+  }
   *out = e;
   return 0;
+}
+
+int mmb_create(const mmb_model_spec* spec, int device, mmb_engine** out) {
+  if (spec && spec->model == MMB_MODEL_IR)
+    return fail(nullptr, MMB_E_ARG, "node-IR models are created with mmb_create_ir");
+  return create_impl(spec, nullptr, device, out);
+}
+
+// Host-side validation of a node IR: every code word, slot, pool range and gather index is
+// checked against the node lengths, so no kernel can address outside its LDS row or the pool.
+static int ir_check_expr(const mmb_ir_model* ir, int pc, int len, int* depth) {
+  int sp = 0, mx = 0;
+  for (int steps = 0; steps < ir->ncode + 1; ++steps, ++pc) {
+    if (pc < 0 || pc >= ir->ncode) return -1;
+    const int w = ir->code[pc];
+    const int op = (int)((uint32_t)w >> 24), arg = w & 0xffffff;
+    if (op == MMB_IR_OP_END) {
+      if (sp != 1) return -1;
+      *depth = std::max(*depth, mx);
+      return 0;
+    }
+    if (op < 16) {
+      switch (op) {
+        case MMB_IR_OP_CONST: if (arg >= ir->nconst) return -1; break;
+        case MMB_IR_OP_VAL: if (arg >= ir->nvalues) return -1; break;
+        case MMB_IR_OP_VALI: if ((int64_t)arg + len > ir->nvalues) return -1; break;
+        case MMB_IR_OP_VALG: {
+          if (++pc >= ir->ncode) return -1;
+          const int64_t w2 = ir->code[pc];
+          if (w2 < 0 || w2 + len > ir->npool) return -1;
+          for (int i = 0; i < len; ++i) {
+            const double q = ir->pool[w2 + i];
+            if (!(q >= 0.0) || q != (double)(int64_t)q || (int64_t)arg + (int64_t)q >= ir->nvalues) return -1;
+          }
+          break;
+        }
+        case MMB_IR_OP_DATA: if ((int64_t)arg + len > ir->npool) return -1; break;
+        case MMB_IR_OP_DATAS: if ((int64_t)arg >= ir->npool) return -1; break;
+        default: return -1;
+      }
+      ++sp;
+      mx = std::max(mx, sp);
+    } else if (op < 32) {
+      if (op > MMB_IR_OP_DIV || sp < 2) return -1;
+      --sp;
+    } else if (op > MMB_IR_OP_ABS || sp < 1) {
+      return -1;
+    }
+  }
+  return -1;
+}
+
+int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out) {
+  if (!spec || !ir || !out) return fail(nullptr, MMB_E_ARG, "null argument");
+  if (spec->model != MMB_MODEL_IR) return fail(nullptr, MMB_E_ARG, "spec->model must be MMB_MODEL_IR");
+  if (ir->nvalues < 1 || ir->nvalues > MMB_IR_MAX_VALUES)
+    return fail(nullptr, MMB_E_UNSUPPORTED, "node IR: 1 <= nvalues <= %d", MMB_IR_MAX_VALUES);
+  if (ir->nnodes < 1 || !ir->nodes || ir->ncode < 1 || !ir->code || ir->npool < 0 || (ir->npool > 0 && !ir->pool) ||
+      ir->nconst < 0 || (ir->nconst > 0 && !ir->consts) || ir->nmon < 0 || (ir->nmon > 0 && !ir->mon))
+    return fail(nullptr, MMB_E_ARG, "node IR: missing tables");
+  if (ir->stack < 1 || ir->stack > MMB_IR_MAX_STACK)
+    return fail(nullptr, MMB_E_ARG, "node IR: stack depth must be 1..%d", MMB_IR_MAX_STACK);
+  int depth = 0;
+  for (int n = 0; n < ir->nnodes; ++n) {
+    const mmb_ir_node& N = ir->nodes[n];
+    if (N.family < MMB_IR_NORMAL || N.family > MMB_IR_LOGICAL || N.len < 1)
+      return fail(nullptr, MMB_E_ARG, "node IR: node %d has a bad family or length", n);
+    if (N.family != MMB_IR_LOGICAL) {
+      const int64_t end = (int64_t)N.off + N.len;
+      if (N.off < 0 || end > (N.fixed ? ir->npool : (int64_t)ir->nvalues))
+        return fail(nullptr, MMB_E_ARG, "node IR: node %d values out of range", n);
+    }
+    if (N.family >= MMB_IR_BINOMIAL && N.family <= MMB_IR_BERNOULLI && !N.fixed)
+      return fail(nullptr, MMB_E_UNSUPPORTED, "node IR: discrete node %d must be fixed (observed)", n);
+    if (N.cterm >= 0 && (int64_t)N.cterm + N.len > ir->npool)
+      return fail(nullptr, MMB_E_ARG, "node IR: node %d constant term out of range", n);
+    const int nexpr = N.family == MMB_IR_LOGICAL || N.family == MMB_IR_EXPONENTIAL || N.family == MMB_IR_POISSON ||
+                              N.family == MMB_IR_BERNOULLI ? 1 : 2;
+    for (int k = 0; k < 3; ++k) {
+      if (k >= nexpr) {
+        if (N.expr[k] >= 0) return fail(nullptr, MMB_E_ARG, "node IR: node %d has extra parameters", n);
+        continue;
+      }
+      if (ir_check_expr(ir, N.expr[k], N.family == MMB_IR_ISONORMAL && k == 1 ? 1 : N.len, &depth))
+        return fail(nullptr, MMB_E_ARG, "node IR: node %d parameter %d has invalid code", n, k);
+    }
+  }
+  if (depth > ir->stack) return fail(nullptr, MMB_E_ARG, "node IR: stack depth %d exceeds %d", depth, ir->stack);
+  for (int q = 0; q < ir->nmon; ++q)
+    if (ir->mon[q] < 0 || ir->mon[q] >= ir->nnodes) return fail(nullptr, MMB_E_ARG, "node IR: bad monitored node");
+  if (spec->nblocks < 1 || spec->nblocks > MMB_MAX_BLOCKS)
+    return fail(nullptr, MMB_E_ARG, "nblocks must be in 1..%d", MMB_MAX_BLOCKS);
+  for (int b = 0; b < spec->nblocks; ++b) {
+    const mmb_ir_block& B = ir->blocks[b];
+    if (B.nterms < 1 || B.nterms > MMB_IR_MAX_TERMS) return fail(nullptr, MMB_E_ARG, "node IR: block %d terms", b);
+    for (int t = 0; t < B.nterms; ++t)
+      if (B.term[t] < 0 || B.term[t] >= ir->nnodes || ir->nodes[B.term[t]].family == MMB_IR_LOGICAL)
+        return fail(nullptr, MMB_E_ARG, "node IR: block %d term %d invalid", b, t);
+  }
+  return create_impl(spec, ir, device, out);
 }
 
 static void free_dev(mmb_engine* e) {
@@ -351,6 +516,11 @@ void mmb_destroy(mmb_engine* e) {
 #endif
   free_dev(e);
   if (e->d_data) (void)hipFree(e->d_data);
+  {
+    void* ip[] = {e->d_ir_nodes, e->d_ir_code, e->d_ir_mon, e->d_ir_const, e->d_ir_pool, e->d_ir_blocks};
+    for (void* q : ip)
+      if (q) (void)hipFree(q);
+  }
   if (e->lg_X) (void)hipFree(e->lg_X);
   if (e->lg_y) (void)hipFree(e->lg_y);
   if (e->lg_hcount) (void)hipHostFree(e->lg_hcount);
@@ -436,7 +606,7 @@ static void to_device_layout(const mmb_engine* e, const double* v, double* dv) {
     std::fill(dv, dv + e->VS, 0.0);
     for (int i = 0; i < 30; ++i) { dv[i] = v[1 + i]; dv[32 + i] = v[33 + i]; }
     dv[64] = v[0]; dv[65] = v[31]; dv[66] = v[32]; dv[67] = v[63]; dv[68] = v[64];
-  } else if (e->model == MMB_MODEL_LOGISTIC) {
+  } else if (e->model == MMB_MODEL_LOGISTIC || e->model == MMB_MODEL_IR) {
     std::fill(dv, dv + e->VS, 0.0);
     for (int i = 0; i < e->P; ++i) dv[i] = v[i];
   } else {
@@ -447,7 +617,7 @@ static void from_device_layout(const mmb_engine* e, const double* dv, double* v)
   if (e->model == MMB_MODEL_RATS) {
     for (int i = 0; i < 30; ++i) { v[1 + i] = dv[i]; v[33 + i] = dv[32 + i]; }
     v[0] = dv[64]; v[31] = dv[65]; v[32] = dv[66]; v[63] = dv[67]; v[64] = dv[68];
-  } else if (e->model == MMB_MODEL_LOGISTIC) {
+  } else if (e->model == MMB_MODEL_LOGISTIC || e->model == MMB_MODEL_IR) {
     for (int i = 0; i < e->P; ++i) v[i] = dv[i];
   } else {
     v[0] = dv[0]; v[1] = dv[1]; v[2] = dv[2];
@@ -510,6 +680,7 @@ static int upload_blocks(mmb_engine* e) {
     d.t_sigma = h.sigma; d.t_accept = h.accept; d.t_m = h.m; d.t_flags = h.flags;
     d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_nuts = h.nuts; d.t_nfr = h.nfr;
     d.t_hmc = h.hmc;
+    d.ir_blk = (int32_t)b;
   }
   if (!e->d_blocks) HIPCHK(e, hipMalloc(&e->d_blocks, MMB_MAX_BLOCKS * sizeof(DBlock)));
   HIPCHK(e, hipMemcpy(e->d_blocks, db.data(), db.size() * sizeof(DBlock), hipMemcpyHostToDevice));
@@ -570,6 +741,9 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
       if (e->model == MMB_MODEL_LINE) {
         const size_t fr = (size_t)NutsFrames<Mdl<MMB_MODEL_LINE>::G * Mdl<MMB_MODEL_LINE>::R>::DBL;
         HIPCHK(e, dalloc(&h.nfr, K * fr));
+      } else if (e->model == MMB_MODEL_IR) {
+        const size_t fr = (size_t)NutsFrames<Mdl<MMB_MODEL_IR>::G * Mdl<MMB_MODEL_IR>::R>::DBL;
+        HIPCHK(e, dalloc(&h.nfr, K * fr));
       }
     } else if (h.spec.sampler == MMB_SAMPLER_HMC || h.spec.sampler == MMB_SAMPLER_MALA) {
       HIPCHK(e, dalloc(&h.hmc, K * 2));
@@ -618,7 +792,15 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.vals = e->d_vals;
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
-  if (e->model == MMB_MODEL_RATS) {
+  if (e->model == MMB_MODEL_IR) {
+    A.ir_nodes = e->d_ir_nodes; A.ir_code = e->d_ir_code; A.ir_const = e->d_ir_const;
+    A.ir_pool = e->d_ir_pool; A.ir_blocks = e->d_ir_blocks; A.ir_mon = e->d_ir_mon;
+    A.ir_nmon = (int32_t)e->ir_mon.size();
+    A.ir_pmon = e->pmon;
+    A.ir_vs = e->VS;
+    A.ir_amm = (e->kinds & (1u << MMB_SAMPLER_AMM)) ? Mdl<MMB_MODEL_IR>::AMM_DBL : 0;
+    A.ir_lds = A.ir_amm + 2 * e->VS + (e->ir_stack + 1) * Mdl<MMB_MODEL_IR>::G;
+  } else if (e->model == MMB_MODEL_RATS) {
     double s = 0.0;
     for (int i = 0; i < 5; ++i) s += e->x[i];
     A.xbar = s / 5.0;
@@ -632,7 +814,7 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
 static int iters_per_launch(const mmb_engine* e) {
   const char* s = std::getenv("MMB_ITERS_PER_LAUNCH");
   if (s && std::atoi(s) > 0) return std::atoi(s);
-  return e->model == MMB_MODEL_RATS ? 8 : 64;
+  return e->model == MMB_MODEL_RATS ? 8 : e->model == MMB_MODEL_IR ? 16 : 64;
 }
 
 template <class T>

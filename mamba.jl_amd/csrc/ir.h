@@ -1,0 +1,230 @@
+// ir.h — the generic node-IR model of the sweep kernel.
+//
+// A Mamba Model DAG (src/model/model.jl:5-27, src/model/dependent.jl:75-152) lowered by the
+// host (mamba.jl_amd/ir.py) into mmb_ir_node records (include/mamba_hip.h) whose
+// distribution parameters are stack-code expressions over the chain state, the data pool
+// and the element index i.  One chain per 32-lane group (two chains per wave64), element i
+// of a node in lane i % 32, so the samplers of samplers.h run unchanged (R = 1, d <= 32;
+// the AMM factorization is pchol32).  LDS per chain:
+//
+//   [AMM scratch (schemes with AMM)] [cur: chain state] [prop: state + the block's
+//   candidate x] [expression stack: depth x 32 doubles]
+//
+// logpdf!(m, x, block, transform) (src/model/simulation.jl:77-90): relist x into `prop`
+// (invlink when transformed, transformdistribution.jl:6-93), then the block's terms —
+// params \ targets in block order, then targets in topological order — each a node
+// logpdf_sub (distributionstruct.jl:136-168: per element insupport ? logpdf (+ Jacobian)
+// : -Inf; lane partials in element order, then the 32-lane butterfly), with the early exit
+// on a non-finite running sum (simulation.jl:64,84).  NUTS / HMC / MALA use Calculus'
+// forward difference like the reference's gradlogpdf! (simulation.jl:47-51,
+// sampler.jl:106-111): d + 1 logpdf! per gradient.
+#pragma once
+#include "device.h"
+
+template <class T>
+__device__ __forceinline__ const T& ir_const_ref(const T* p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const T*)&((const __attribute__((address_space(4))) T*)p)[i];
+#else
+  return p[i];
+#endif
+}
+
+template <>
+struct Mdl<MMB_MODEL_IR> {
+  static constexpr int G = 32, R = 1, DMAX = 32, DP = 32, TP = 528, VS = 0, PMON = 0;
+  // AMM scratch: mat[TP] | z2 | vv | mv | ia, then pchol32's reciprocal slot prow[DMAX]
+  static constexpr int AMM_DBL = TP + 4 * DP + 2;
+  static constexpr int LDS_DBL = 0;  // runtime layout: lds_stride()
+  struct St {
+    double* cur;                 // chain state (LDS)
+    double* prop;                // state with the block candidate written in (LDS)
+    double* stk;                 // expression stack spills (LDS)
+    const mmb_ir_node* nodes;    // node table (uniform)
+  };
+  struct Lc { int dummy; };
+  __host__ __device__ static int lds_stride(const SweepArgs& A) { return A.ir_lds; }
+
+  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc&, double* lds) {
+    s.cur = lds + A.ir_amm;
+    s.prop = s.cur + A.ir_vs;
+    s.stk = s.prop + A.ir_vs;
+    s.nodes = A.ir_nodes;
+    const double* v = A.vals + (size_t)c * A.ir_vs;
+    for (int j = lane; j < A.ir_vs; j += G) {
+      const double t = v[j];
+      s.cur[j] = t;
+      s.prop[j] = t;
+    }
+    grp_sync();
+  }
+  __device__ __forceinline__ static void store(const SweepArgs& A, int c, int lane, const St& s) {
+    grp_sync();
+    double* v = A.vals + (size_t)c * A.ir_vs;
+    for (int j = lane; j < A.ir_vs; j += G) v[j] = s.cur[j];
+  }
+  __device__ __forceinline__ static void stash(double*, const St&, int) {}  // state already in LDS
+  __device__ __forceinline__ static void unstash(const double*, St&, int) {}
+
+  // ---- expressions: stack code, top of stack in a register, spills in this lane's LDS column
+  __device__ static double ev(const SweepArgs& A, int pc, int i, const double* vals, double* stk, int lane) {
+    double acc = 0.0;
+    int sp = 0;
+    for (;; ++pc) {
+      const int w = ir_const_ref(A.ir_code, pc);
+      const int op = (int)((uint32_t)w >> 24), arg = w & 0xffffff;
+      if (op == MMB_IR_OP_END) return acc;
+      if (op < 16) {
+        double v;
+        if (op == MMB_IR_OP_CONST) v = A.ir_const[arg];
+        else if (op == MMB_IR_OP_VAL) v = vals[arg];
+        else if (op == MMB_IR_OP_VALI) v = vals[arg + i];
+        else if (op == MMB_IR_OP_VALG) {
+          ++pc;
+          v = vals[arg + (int)A.ir_pool[ir_const_ref(A.ir_code, pc) + i]];
+        } else if (op == MMB_IR_OP_DATA) v = A.ir_pool[arg + i];
+        else v = A.ir_pool[arg];  // MMB_IR_OP_DATAS
+        stk[sp * G + lane] = acc;
+        ++sp;
+        acc = v;
+      } else if (op < 32) {
+        --sp;
+        const double l = stk[sp * G + lane];
+        if (op == MMB_IR_OP_ADD) acc = l + acc;
+        else if (op == MMB_IR_OP_SUB) acc = l - acc;
+        else if (op == MMB_IR_OP_MUL) acc = l * acc;
+        else acc = l / acc;  // MMB_IR_OP_DIV
+      } else {
+        acc = mmb_ir_unary(op, acc);
+      }
+    }
+  }
+
+  // logpdf(node[, transform]) (dependent.jl:207-213 -> logpdf_sub), group-uniform result
+  __device__ static double node_lp(const SweepArgs& A, int n, const double* vals, double* stk,
+                                   const Grp<G>& g, int tr) {
+    const mmb_ir_node& N = ir_const_ref(A.ir_nodes, n);
+    const double* src = N.fixed ? A.ir_pool + N.off : vals + N.off;
+    const int lane = g.lane;
+    if (N.family == MMB_IR_ISONORMAL) {  // MvNormal(mu, sigma): PDMats ScalMat, insupport = all finite
+      const double sig = ev(A, N.expr[1], 0, vals, stk, lane);
+      double ss = 0.0, bad = 0.0;
+      for (int i = lane; i < N.len; i += G) {
+        const double x = src[i];
+        const double r = x - ev(A, N.expr[0], i, vals, stk, lane);
+        ss = ss + r * r;
+        bad = isfinite(x) ? bad : 1.0;
+      }
+      g.sum2(ss, bad);
+      return bad != 0.0 ? -__builtin_inf() : d_iso(N.len, sig, ss);
+    }
+    double acc = 0.0;
+    for (int i = lane; i < N.len; i += G) {
+      const double a = N.expr[0] >= 0 ? ev(A, N.expr[0], i, vals, stk, lane) : 0.0;
+      const double b = N.expr[1] >= 0 ? ev(A, N.expr[1], i, vals, stk, lane) : 0.0;
+      const double ct = N.cterm >= 0 ? A.ir_pool[N.cterm + i] : 0.0;
+      acc = acc + mmb_ir_lp(N.family, src[i], a, b, ct, tr, N.lo, N.hi);
+    }
+    return g.sum(acc);
+  }
+
+  // element e of the block vector: its state slot and its node's link
+  __device__ __forceinline__ static int elem(const St& s, const DBlock& B, int e, int* lk, double* lo, double* hi) {
+    int base = 0, slot = 0;
+    *lk = 0; *lo = 0.0; *hi = 0.0;
+    for (int a = 0; a < B.nn; ++a) {
+      const mmb_ir_node& N = ir_const_ref(s.nodes, B.nodes[a]);
+      if (e >= base && e < base + N.len) {
+        slot = N.off + e - base;
+        *lk = mmb_ir_link_kind(N.family);
+        *lo = N.lo; *hi = N.hi;
+      }
+      base += N.len;
+    }
+    return slot;
+  }
+  // unlist(block, transform) (simulation.jl:110-163): lane e holds element e
+  __device__ __forceinline__ static void unlist(const DBlock& B, const St& s, int lane, double* x) {
+    x[0] = 0.0;
+    if (lane < B.d) {
+      int lk; double lo, hi;
+      const double v = s.cur[elem(s, B, lane, &lk, &lo, &hi)];
+      x[0] = B.transform ? mmb_ir_link(lk, v, lo, hi) : v;
+    }
+  }
+  // write x (invlinked when transformed) at the block's slots of dst (and dst2)
+  __device__ __forceinline__ static void put(const DBlock& B, const St& s, int lane, const double* x, double* dst,
+                                             double* dst2) {
+    grp_sync();
+    if (lane < B.d) {
+      int lk; double lo, hi;
+      const int slot = elem(s, B, lane, &lk, &lo, &hi);
+      const double v = B.transform ? mmb_ir_invlink(lk, x[0], lo, hi) : x[0];
+      dst[slot] = v;
+      if (dst2) dst2[slot] = v;
+    }
+    grp_sync();
+  }
+  // relist (m[params] = relist(block, x)): the committed state, mirrored into prop
+  __device__ __forceinline__ static void relist(const DBlock& B, St& s, const Grp<G>& g, const double* x) {
+    put(B, s, g.lane, x, s.cur, s.prop);
+  }
+
+  struct Prep {};
+  __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
+  // logpdf!(m, x, block, transform)
+  __device__ static double logf(const SweepArgs& A, const DBlock& B, const St& s, const Lc&, const Grp<G>& g,
+                                const double* x) {
+    put(B, s, g.lane, x, s.prop, nullptr);
+    const mmb_ir_block& IB = ir_const_ref(A.ir_blocks, B.ir_blk);
+    double lp = 0.0;
+    for (int t = 0; t < IB.nterms; ++t) {
+      lp += node_lp(A, IB.term[t], s.prop, s.stk, g, IB.trans[t] ? B.transform : 0);
+      if (!isfinite(lp)) break;
+    }
+    return lp;
+  }
+  __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep&, const St& s,
+                                                  const Lc& l, const Grp<G>& g, const double* x) {
+    return logf(A, B, s, l, g, x);
+  }
+  // logpdfgrad!(block, x, :forward) (sampler.jl:106-111): Calculus forward differences,
+  // epsilon = sqrt(eps()) * max(1, |x_i|); non-finite gradient entries -> 0
+  __device__ static double logf_grad(const SweepArgs& A, const DBlock& B, const St& s, const double* x,
+                                     double* gr) {
+    Grp<G> g;
+    const Lc l{};
+    const double fx = logf(A, B, s, l, g, x);
+    double gi = 0.0;
+    for (int e = 0; e < B.d; ++e) {
+      const bool own = g.lane == e;
+      const double ax = fabs(x[0]);
+      const double eps = 0x1p-26 * (isnan(ax) ? ax : (ax > 1.0 ? ax : 1.0));
+      double xe[1] = {own ? x[0] + eps : x[0]};
+      const double fp = logf(A, B, s, l, g, xe);
+      if (own) gi = (fp - fx) / eps;
+    }
+    gr[0] = (g.lane < B.d && isfinite(gi)) ? gi : 0.0;
+    return fx;
+  }
+
+  __device__ __forceinline__ static int gibbs_draw_kind(const DBlock&, double* a) { *a = 0.0; return 0; }
+  __device__ __forceinline__ static void gibbs(const SweepArgs&, const DBlock&, St&, const Lc&, const Grp<G>&,
+                                               const mmb_rng*, const mmb_rng*, const mmb_rng*, double) {}
+
+  // sim[i, :, 1] = unlist(m, true) (mcmc.jl:76-77): monitored nodes in Chains order; logicals
+  // are evaluated on the current state (their update! runs after every block, simulation.jl:102)
+  __device__ static void write_draws(const SweepArgs& A, const St& s, const Grp<G>& g, int64_t row, int c) {
+    grp_sync();
+    int col = 0;
+    for (int q = 0; q < A.ir_nmon; ++q) {
+      const mmb_ir_node& N = ir_const_ref(A.ir_nodes, ir_const_ref(A.ir_mon, q));
+      for (int i = g.lane; i < N.len; i += G) {
+        const double v = N.family == MMB_IR_LOGICAL ? ev(A, N.expr[0], i, s.cur, s.stk, g.lane)
+                                                    : (N.fixed ? A.ir_pool + N.off : s.cur + N.off)[i];
+        A.draws[(size_t)(row * A.ir_pmon + col + i) * A.K + c] = v;
+      }
+      col += N.len;
+    }
+  }
+};

@@ -22,7 +22,8 @@ struct Mdl<MMB_MODEL_RATS> {
   struct St { double a, b, s2c, mua, s2a, mub, s2b; };
   struct Lc { const double* y; };  // this lane's 5 observations (global, L1-resident)
 
-  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc& l) {
+  __host__ __device__ static int lds_stride(const SweepArgs&) { return LDS_DBL; }
+  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc& l, double*) {
     const double* v = A.vals + (size_t)c * VS;
     s.a = v[lane];
     s.b = v[32 + lane];
@@ -39,6 +40,15 @@ struct Mdl<MMB_MODEL_RATS> {
     out[0] = s.s2c;
     out[1] = s.mub;
     out[2] = s.mua - A.xbar * s.mub;  // alpha0 = mu_alpha - xbar * mu_beta (rats.jl:65-67)
+  }
+  // sim[i, :, 1] = unlist(m, true) for a kept iteration (mcmc.jl:76-77): lane 0 of the group
+  __device__ __forceinline__ static void write_draws(const SweepArgs& A, const St& s, const Grp<G>& g,
+                                                     int64_t row, int c) {
+    if (g.lane != 0) return;
+    double mon[PMON];
+    monitored(A, s, mon);
+#pragma unroll
+    for (int j = 0; j < PMON; ++j) A.draws[(size_t)(row * PMON + j) * A.K + c] = mon[j];
   }
   __device__ __forceinline__ static bool is_vec(int node) { return node == MMB_RATS_ALPHA || node == MMB_RATS_BETA; }
   __device__ __forceinline__ static bool positive(int node) {
@@ -261,7 +271,8 @@ struct Mdl<MMB_MODEL_LINE> {
     s.v[0] = q[0]; s.v[1] = q[1]; s.v[2] = q[2];
   }
 
-  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int, St& s, Lc&) {
+  __host__ __device__ static int lds_stride(const SweepArgs&) { return LDS_DBL; }
+  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int, St& s, Lc&, double*) {
     const double* v = A.vals + (size_t)c * VS;
     s.v[0] = v[0]; s.v[1] = v[1]; s.v[2] = v[2];
   }
@@ -271,6 +282,11 @@ struct Mdl<MMB_MODEL_LINE> {
   }
   __device__ __forceinline__ static void monitored(const SweepArgs&, const St& s, double* out) {
     out[0] = s.v[0]; out[1] = s.v[1]; out[2] = s.v[2];
+  }
+  __device__ __forceinline__ static void write_draws(const SweepArgs& A, const St& s, const Grp<G>&,
+                                                     int64_t row, int c) {
+#pragma unroll
+    for (int j = 0; j < PMON; ++j) A.draws[(size_t)(row * PMON + j) * A.K + c] = s.v[j];
   }
   __device__ __forceinline__ static double pick(const St& s, int vi) {
     return vi == 0 ? s.v[0] : vi == 1 ? s.v[1] : s.v[2];

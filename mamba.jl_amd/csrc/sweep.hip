@@ -8,6 +8,7 @@
 // element fastest, coalesced per lane group); the AMM covariance and its
 // pivoted Cholesky factor are staged in LDS.
 #include "samplers.h"
+#include "ir.h"
 
 #ifdef MMB_PHASE_PROF
 #include <cstdio>
@@ -28,7 +29,7 @@ void mmb_prof_dump() {
 // measured 12 % faster than 3 despite spills); line has 64 waves in all, so it keeps the
 // whole register budget (no spills).
 template <int MODEL>
-constexpr int sweep_waves() { return MODEL == MMB_MODEL_RATS ? MMB_SWEEP_WAVES : 1; }
+constexpr int sweep_waves() { return MODEL == MMB_MODEL_RATS ? MMB_SWEEP_WAVES : MODEL == MMB_MODEL_IR ? 2 : 1; }
 
 // KINDS: bitmask (1 << mmb_sampler_kind) of the sampler kinds present in the scheme; the
 // other block paths are compiled out (register/SGPR allocation is per kernel).
@@ -41,10 +42,10 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
   const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
   if (c >= A.K) return;  // whole lane groups exit together
   Grp<G> g;
-  double* lds = smem + (size_t)(threadIdx.x / G) * M::LDS_DBL;
+  double* lds = smem + (size_t)(threadIdx.x / G) * M::lds_stride(A);
   typename M::St s;
   typename M::Lc l;
-  M::load(A, c, g.lane, s, l);
+  M::load(A, c, g.lane, s, l, lds);
   const uint32_t chain = A.chain_offset + (uint32_t)c;
 #ifdef MMB_PHASE_PROF
   if ((threadIdx.x & 63) == 0)
@@ -108,12 +109,9 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
       mmb_prof_lds()[9] += 1;
     }
 #endif
-    if (A.draws && it > A.burnin && (it - A.burnin) % A.thin == 0 && g.lane == 0) {
+    if (A.draws && it > A.burnin && (it - A.burnin) % A.thin == 0) {
       const int64_t row = (it - A.burnin) / A.thin - 1 - A.kept_origin;
-      double mon[M::PMON];
-      M::monitored(A, s, mon);
-#pragma unroll
-      for (int j = 0; j < M::PMON; ++j) A.draws[(size_t)(row * M::PMON + j) * A.K + c] = mon[j];
+      M::write_draws(A, s, g, row, c);
     }
   }
   M::store(A, c, g.lane, s);
@@ -129,13 +127,14 @@ constexpr unsigned K_GRAD = (1u << MMB_SAMPLER_NUTS) | (1u << MMB_SAMPLER_HMC) |
 constexpr unsigned K_ALL_GRAD = K_ALL | K_GRAD;
 constexpr unsigned K_GIBBS_AMM = (1u << MMB_SAMPLER_AMM) | (1u << MMB_SAMPLER_GIBBS);
 constexpr unsigned K_SLICE_AMWG = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_SLICE);
+constexpr unsigned K_IR = (1u << MMB_SAMPLER_AMWG) | (1u << MMB_SAMPLER_AMM) | (1u << MMB_SAMPLER_SLICE) | K_GRAD;
 
 template <int MODEL, unsigned KINDS>
 static hipError_t launch(const SweepArgs& A, hipStream_t st, int threads) {
   using M = Mdl<MODEL>;
   const int per_block = threads / M::G;
   const int blocks = (A.K + per_block - 1) / per_block;
-  const size_t lds = (size_t)per_block * M::LDS_DBL * sizeof(double);
+  const size_t lds = (size_t)per_block * M::lds_stride(A) * sizeof(double);
   hipLaunchKernelGGL((sweep_kernel<MODEL, KINDS>), dim3(blocks), dim3(threads), lds, st, A);
   return hipGetLastError();
 }
@@ -151,6 +150,7 @@ hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipSt
     if ((kinds & ~K_SLICE_AMWG) == 0) return launch<MMB_MODEL_RATS, K_SLICE_AMWG>(A, st, TB);
     return launch<MMB_MODEL_RATS, K_ALL>(A, st, TB);
   }
+  if (model == MMB_MODEL_IR) return launch<MMB_MODEL_IR, K_IR>(A, st, 128);
   if (model == MMB_MODEL_LINE) {
     if (kinds & K_GRAD) return launch<MMB_MODEL_LINE, K_ALL_GRAD>(A, st, 64);
     return launch<MMB_MODEL_LINE, K_ALL>(A, st, 64);

@@ -22,7 +22,11 @@ class Engine:
         self.model = model
         self.spec = model.spec()
         h = C.c_void_p()
-        rc = self.lib.mmb_create(C.byref(self.spec), int(device), C.byref(h))
+        if model.kind == abi.MMB_MODEL_IR:  # generic node IR (ir.py)
+            self.ir = model.ir()
+            rc = self.lib.mmb_create_ir(C.byref(self.spec), C.byref(self.ir), int(device), C.byref(h))
+        else:
+            rc = self.lib.mmb_create(C.byref(self.spec), int(device), C.byref(h))
         if rc != 0:
             raise RuntimeError(f"mmb_create failed ({abi.ERRORS.get(rc, rc)}): "
                                f"{self.lib.mmb_last_error(None).decode()}")

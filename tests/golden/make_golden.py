@@ -18,6 +18,8 @@ Fixtures (all small JSON, committed):
                     (beta grid x analytic s2 marginal); statistical target for the samplers.
   rats_published.json  summaries printed in doc/examples/rats.rst:37-52 (10k iters,
                     burnin 2500, thin 2, 2 chains, the reference Slice+AMWG scheme).
+  ir_published.json  "Empirical Posterior Estimates" (Mean, SD, MCSE) printed in
+                    doc/examples/{seeds,pumps,surgical,dyes}.rst for the node-IR examples.
 """
 import json
 import os
@@ -45,6 +47,22 @@ RATS_Y = np.array([
     132, 185, 237, 286, 331, 160, 207, 257, 303, 345, 169, 216, 261, 295, 333,
     157, 205, 248, 289, 316, 137, 180, 219, 258, 291, 153, 200, 244, 286, 324], dtype=float)
 RATS_X = np.array([8.0, 15.0, 22.0, 29.0, 36.0])
+
+
+def ir_published():
+    """Mean / SD / MCSE columns of the first summary table of each example's .rst."""
+    out = {}
+    for ex in ("seeds", "pumps", "surgical", "dyes"):
+        lines = open(os.path.join(REF, "doc", "examples", ex + ".rst")).read().splitlines()
+        i = next(k for k, ln in enumerate(lines) if "Empirical Posterior Estimates" in ln) + 2
+        rows = {}
+        while i < len(lines) and lines[i].strip():
+            f = lines[i].split()
+            rows[f[0]] = {"mean": float(f[1]), "sd": float(f[2]), "mcse": float(f[4])}
+            i += 1
+        it = next(ln for ln in lines if "Iterations =" in ln).split("=")[1].strip()
+        out[ex] = {"iterations": it, "rows": rows}
+    return out
 
 
 def philox():
@@ -281,6 +299,7 @@ def main():
     dump("coda_line.json", coda())
     dump("line_posterior.json", line_posterior())
     dump("rats_published.json", rats_published())
+    dump("ir_published.json", ir_published())
 
 
 if __name__ == "__main__":

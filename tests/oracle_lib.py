@@ -45,9 +45,20 @@ class Oracle:
         for f in ("orc_uniform", "orc_normal"):
             getattr(L, f).restype = C.c_double
             getattr(L, f).argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_set_ir.argtypes = [C.c_void_p]
+        L.orc_lgamma.restype = C.c_double
+        L.orc_lgamma.argtypes = [C.c_double]
+        L.orc_ir_elem_lp.restype = C.c_double
+        L.orc_ir_elem_lp.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_int,
+                                     C.c_double, C.c_double]
         L.orc_gamma.restype = C.c_double
         L.orc_gamma.argtypes = [C.c_double, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
         self.L = L
+
+    def _ir(self, model):
+        """Node-IR models: hand the lowered mmb_ir_model to the oracle (orc_set_ir)."""
+        if model.kind == self.abi.MMB_MODEL_IR:
+            self.L.orc_set_ir(C.addressof(model.ir()))
 
     @staticmethod
     def _data(model):
@@ -57,6 +68,7 @@ class Oracle:
         return arrs, ptrs, ns
 
     def new_state(self, model, init):
+        self._ir(model)
         spec = model.spec()
         arrs, ptrs, ns = self._data(model)
         K = init.shape[0]
@@ -71,6 +83,7 @@ class Oracle:
 
     def run(self, model, state, iters, burnin=0, thin=1, model_burnin=None, chain_offset=0, seed=1,
             nthreads=1, draws=True):
+        self._ir(model)
         spec = model.spec()
         arrs, ptrs, ns = self._data(model)
         K = state["values"].shape[0]
@@ -92,6 +105,7 @@ class Oracle:
         return np.asfortranarray(dr[:nk])
 
     def block_logpdf(self, model, values, block, x, grad=False):
+        self._ir(model)
         spec = model.spec()
         arrs, ptrs, ns = self._data(model)
         v = np.ascontiguousarray(values, dtype=np.float64)
