@@ -16,6 +16,10 @@ Other BASELINE configs (reported in DESIGN.md, not the metric line):
   --workload line_amm   configs[1]: line regression, AMM, 4096 chains per GPU
   --workload logistic   configs[3]: logistic N=10000 p=50, NUTS, 4096 chains per GPU
                         (roofline bound "mfma": algorithmic 4*N*p flops per gradient)
+  --workload seeds_ir   node IR: doc/examples/seeds.jl lowered generically,
+                        its own scheme AMM(4) + AMWG(b, 21) + AMWG(s2), 16384 chains per GPU
+  --workload rats_ir    node IR: the rats model + the reference Slice/AMWG scheme lowered
+                        generically (compare: --workload rats --scheme reference, hand-fused)
 """
 import argparse
 import json
@@ -37,14 +41,15 @@ def parse():
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--chains", type=int, default=None, help="chains per GPU")
-    p.add_argument("--workload", default="rats", choices=["rats", "line_amm", "logistic"])
+    p.add_argument("--workload", default="rats", choices=["rats", "line_amm", "logistic", "seeds_ir", "rats_ir"])
     p.add_argument("--thin", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--scheme", default="gibbs_amm",
                    help="gibbs_amm (metric config) | reference | ablations: amm_noadapt, gibbs_only")
     a = p.parse_args()
-    dflt = {"rats": (CHAINS_PER_GPU, 400, 200), "line_amm": (4096, 2000, 500), "logistic": (4096, 100, 100)}
+    dflt = {"rats": (CHAINS_PER_GPU, 400, 200), "line_amm": (4096, 2000, 500), "logistic": (4096, 100, 100),
+            "seeds_ir": (CHAINS_PER_GPU, 160, 80), "rats_ir": (CHAINS_PER_GPU, 64, 32)}
     k, st, wu = dflt[a.workload]
     a.chains = a.chains or k
     a.steps = a.steps if a.steps is not None else st
@@ -110,6 +115,21 @@ def setup_workload(mb, args, rank):
         model.setsamplers([mb.AMM(["beta", "s2"], np.eye(3))])
         init = mb.model.line_init_matrix(K, seed=1000 + rank)
         return model, init, "line AMM (BASELINE configs[1])", {"thin": 1}, "f64"
+    if args.workload == "seeds_ir":
+        ir = mb.ir
+        model = ir.seeds_model().setinputs(ir.SEEDS)
+        model.setsamplers([mb.AMM(["alpha0", "alpha1", "alpha2", "alpha12"], 0.01 * np.eye(4)), mb.AMWG("b", 0.01),
+                           mb.AMWG("s2", 0.1)])
+        rng = np.random.default_rng(1000 + rank)
+        inits = [{**ir.seeds_inits()[k % 2], "b": rng.normal(0.0, 0.1, 21)} for k in range(K)]
+        return (model, model.init_matrix(inits, K), "seeds (doc/examples/seeds.jl) via the node IR: AMM(4) + "
+                "AMWG(b) + AMWG(s2)", {"thin": args.thin}, "f64")
+    if args.workload == "rats_ir":
+        ir = mb.ir
+        model = ir.rats_model().setinputs(ir.rats_inputs()).setsamplers(mb.model.rats_scheme_reference())
+        inits = [{**mb.model.RATS_INITS[k % 2], "y": mb.model.RATS_Y} for k in range(K)]
+        return (model, model.init_matrix(inits, K), "rats via the node IR, reference Slice+AMWG scheme "
+                "(rats.jl:112-116)", {"thin": args.thin}, "f64")
     data, _ = mb.model.logistic_data(10000, 50)
     model = mb.logistic(10000, 50, 10.0)
     model.setinputs(data)
@@ -202,7 +222,8 @@ def main():
                 "avg_launch_ms": kms / launches, "gradients_per_launch": eng.grad_evals() / launches,
                 "gradients_per_chain_update_timed": grads_timed / (K * args.steps)}
     else:
-        W = int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8" if args.workload == "rats" else "64"))
+        W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
+                               "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "64"))
         nroof = max(W * 8, 64)
         eng.run(nroof, burnin=0, thin=thin, model_burnin=0, draws=False, keep_device=False, time_kernels=True)
         kms, launches, units = eng.kernel_time()
@@ -237,6 +258,8 @@ def main():
         "data": ("rats.jl data (real, 30 rats x 5 weeks); synthetic per-chain inits (per-rat LS + jitter)"
                  if args.workload == "rats" else
                  "line.jl data; synthetic inits" if args.workload == "line_amm" else
+                 f"{args.workload[:-3]}.jl data and inits (+ N(0, 0.1^2) jitter on seeds b)" if args.workload.endswith("_ir")
+                 else
                  "synthetic X ~ N(0,1), y ~ Bernoulli(invlogit(X beta_true)) (SURVEY §8d seeds); inits N(0, 0.1^2)"),
         "config": {"workload": desc, "chains_per_gpu": K, "global_chains": K * world, "thin": thin,
                    "parallelism": f"chain-shard x{world}", "collective": "rccl" if backend == "nccl" else backend},
@@ -255,6 +278,9 @@ def main():
         elif args.workload == "line_amm":
             out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds, "line AMM update",
                                                per_thread=256, warm=64)
+        elif args.workload.endswith("_ir"):
+            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds,
+                                               f"{args.workload} node-IR sweep", per_thread=16, warm=16)
         else:
             out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds, "logistic NUTS update",
                                                per_thread=4, warm=20, model_burnin=20)

@@ -1,7 +1,7 @@
 /*
  * mmb_math.h — counter-based RNG and elementary functions used bit for bit by
- * the HIP kernels AND the CPU oracle (oracle/oracle.c includes this header; it
- * is the only product code the oracle shares).
+ * the HIP kernels AND the CPU oracle (oracle/oracle.c includes this header; with
+ * ir_math.h, the node IR's element densities, it is the only product code the oracle shares).
  *
  * Why shared: Mamba.jl's MersenneTwister/ziggurat streams and openlibm cannot
  * be reproduced, so parity is oracle <-> GPU on identical Philox streams
