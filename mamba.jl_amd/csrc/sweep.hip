@@ -28,8 +28,13 @@ void mmb_prof_dump() {
 // Occupancy target per model: rats runs 8192 waves and is latency-bound (4 waves/SIMD
 // measured 12 % faster than 3 despite spills); line has 64 waves in all, so it keeps the
 // whole register budget (no spills).
+#ifndef MMB_IR_WAVES
+#define MMB_IR_WAVES 2  // node IR: min waves per SIMD (register budget 512 / waves)
+#endif
 template <int MODEL>
-constexpr int sweep_waves() { return MODEL == MMB_MODEL_RATS ? MMB_SWEEP_WAVES : MODEL == MMB_MODEL_IR ? 2 : 1; }
+constexpr int sweep_waves() {
+  return MODEL == MMB_MODEL_RATS ? MMB_SWEEP_WAVES : MODEL == MMB_MODEL_IR ? MMB_IR_WAVES : 1;
+}
 
 // KINDS: bitmask (1 << mmb_sampler_kind) of the sampler kinds present in the scheme; the
 // other block paths are compiled out (register/SGPR allocation is per kernel).

@@ -665,3 +665,57 @@ def dyes_model():
 
 def dyes_inputs():
     return {"y": DYES_Y, "batch": np.repeat(np.arange(1, 7), 5).astype(float)}
+
+
+SALM = {"y": [15, 21, 29, 16, 18, 21, 16, 26, 33, 27, 41, 60, 33, 38, 41, 20, 27, 42],  # 3 x 6, column-major
+        "x": [0.0, 10, 33, 100, 333, 1000],                                            # doc/examples/salm.jl:4-11
+        "dose": np.repeat(np.arange(1, 7), 3).astype(float)}                          # column index of y[i, j]
+
+
+def salm_model():
+    """doc/examples/salm.jl:15-47 (Poisson log-linear dose response with plate effects; the
+    node `lambda` is `lam` here, a Python keyword)."""
+    return Model(
+        y=Stochastic(2, lambda alpha, beta, gamma, x, dose, lam:
+                     Poisson(exp(alpha + beta * log(x[dose] + 10) + gamma * x[dose] + lam)), False),
+        alpha=Stochastic(lambda: Normal(0, 1000)),
+        beta=Stochastic(lambda: Normal(0, 1000)),
+        gamma=Stochastic(lambda: Normal(0, 1000)),
+        lam=Stochastic(2, lambda s2: Normal(0, sqrt(s2)), False),
+        s2=Stochastic(lambda: InverseGamma(0.001, 0.001)))
+
+
+def salm_inits():
+    """doc/examples/salm.jl:51-56"""
+    y = SALM["y"]
+    return [{"y": y, "alpha": 0, "beta": 0, "gamma": 0, "s2": 10, "lam": np.zeros(18)},
+            {"y": y, "alpha": 1, "beta": 1, "gamma": 0.01, "s2": 1, "lam": np.zeros(18)}]
+
+
+BLOCKER = {  # doc/examples/blocker.jl:4-17
+    "rt": [3, 7, 5, 102, 28, 4, 98, 60, 25, 138, 64, 45, 9, 57, 25, 33, 28, 8, 6, 32, 27, 22],
+    "nt": [38, 114, 69, 1533, 355, 59, 945, 632, 278, 1916, 873, 263, 291, 858, 154, 207, 251, 151, 174, 209,
+           391, 680],
+    "rc": [3, 14, 11, 127, 27, 6, 152, 48, 37, 188, 52, 47, 16, 45, 31, 38, 12, 6, 3, 40, 43, 39],
+    "nc": [39, 116, 93, 1520, 365, 52, 939, 471, 282, 1921, 583, 266, 293, 883, 147, 213, 122, 154, 134, 218,
+           364, 674]}
+
+
+def blocker_model():
+    """doc/examples/blocker.jl:21-64 (random-effects meta-analysis of 22 trials)."""
+    return Model(
+        rc=Stochastic(1, lambda mu, nc: Binomial(nc, invlogit(mu)), False),
+        rt=Stochastic(1, lambda mu, delta, nt: Binomial(nt, invlogit(mu + delta)), False),
+        mu=Stochastic(1, lambda: Normal(0, 1000), False),
+        delta=Stochastic(1, lambda d, s2: Normal(d, sqrt(s2)), False),
+        delta_new=Stochastic(lambda d, s2: Normal(d, sqrt(s2))),
+        d=Stochastic(lambda: Normal(0, 1000)),
+        s2=Stochastic(lambda: InverseGamma(0.001, 0.001)))
+
+
+def blocker_inits():
+    """doc/examples/blocker.jl:68-73"""
+    b = BLOCKER
+    return [{"rc": b["rc"], "rt": b["rt"], "d": 0, "delta_new": 0, "s2": 1, "mu": np.zeros(22), "delta": np.zeros(22)},
+            {"rc": b["rc"], "rt": b["rt"], "d": 2, "delta_new": 2, "s2": 10, "mu": np.full(22, 2.0),
+             "delta": np.full(22, 2.0)}]

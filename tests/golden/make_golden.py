@@ -19,7 +19,7 @@ Fixtures (all small JSON, committed):
   rats_published.json  summaries printed in doc/examples/rats.rst:37-52 (10k iters,
                     burnin 2500, thin 2, 2 chains, the reference Slice+AMWG scheme).
   ir_published.json  "Empirical Posterior Estimates" (Mean, SD, MCSE) printed in
-                    doc/examples/{seeds,pumps,surgical,dyes}.rst for the node-IR examples.
+                    doc/examples/{seeds,pumps,surgical,dyes,salm,blocker}.rst for the node-IR examples.
 """
 import json
 import os
@@ -52,7 +52,7 @@ RATS_X = np.array([8.0, 15.0, 22.0, 29.0, 36.0])
 def ir_published():
     """Mean / SD / MCSE columns of the first summary table of each example's .rst."""
     out = {}
-    for ex in ("seeds", "pumps", "surgical", "dyes"):
+    for ex in ("seeds", "pumps", "surgical", "dyes", "salm", "blocker"):
         lines = open(os.path.join(REF, "doc", "examples", ex + ".rst")).read().splitlines()
         i = next(k for k, ln in enumerate(lines) if "Empirical Posterior Estimates" in ln) + 2
         rows = {}

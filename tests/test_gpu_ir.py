@@ -1,6 +1,6 @@
 """Node IR on the GPU: the IR sweep kernel through the C ABI
 (mmb_create_ir) against the oracle's restatement of the IR on identical Philox streams, and
-the reference's published posterior summaries (doc/examples/{seeds,pumps,surgical,dyes}.rst)
+the reference's published posterior summaries (doc/examples/{seeds,pumps,surgical,dyes,salm,blocker}.rst)
 reproduced by many chains.  The kernel sums element terms in lane partials + the 32-lane DPP
 butterfly and the oracle mirrors that order, so draws, values and tune are expected
 identical; they are asserted to rtol 1e-9 (discrete tune fields exactly)."""
@@ -39,6 +39,16 @@ def example(mamba, name, K, seed=5, scheme=None):
         inits = [{"y": ir.DYES_Y, "theta": 1500, "s2_within": 1, "s2_between": 1, "mu": [1500] * 6} if k % 2 == 0
                  else {"y": ir.DYES_Y, "theta": 3000, "s2_within": 10, "s2_between": 10, "mu": [3000] * 6}
                  for k in range(K)]
+    elif name == "salm":
+        m = ir.salm_model().setinputs(ir.SALM)
+        m.setsamplers(scheme or [mamba.Slice(["alpha", "beta", "gamma"], [1.0, 1.0, 0.1]),
+                                 mamba.AMWG(["lam", "s2"], 0.1)])                     # salm.jl:60-61
+        inits = [ir.salm_inits()[k % 2] for k in range(K)]
+    elif name == "blocker":
+        m = ir.blocker_model().setinputs(ir.BLOCKER)
+        m.setsamplers(scheme or [mamba.AMWG("mu", 0.1), mamba.AMWG(["delta", "delta_new"], 0.1),
+                                 mamba.Slice(["d", "s2"], 1.0)])                      # blocker.jl:77-79
+        inits = [ir.blocker_inits()[k % 2] for k in range(K)]
     elif name == "line":
         m = ir.line_model().setinputs(mamba.model.LINE_DATA)
         m.setsamplers(scheme)
@@ -63,6 +73,8 @@ CASES = {
     "pumps_slice_uni": ("pumps", None),
     "surgical_nuts_slice": ("surgical", None),
     "dyes_nuts_slice": ("dyes", None),
+    "salm_slice_amwg": ("salm", None),
+    "blocker_amwg_slice": ("blocker", None),
     "dyes_mala_slice": ("dyes", lambda M: [M.MALA("theta", 50.0), M.MALA("mu", 50.0, np.eye(6)),
                                            M.Slice(["s2_within", "s2_between"], 1000.0)]),   # dyes.jl:61-63
     "dyes_hmc_slice": ("dyes", lambda M: [M.HMC("theta", 10.0, 5), M.HMC("mu", 10.0, 5, np.eye(6)),
@@ -92,7 +104,7 @@ def test_ir_rats_reference_scheme_gpu_vs_oracle(mamba, oracle):
     np.testing.assert_allclose(dg, do, rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("name", ["seeds", "pumps", "surgical", "dyes"])
+@pytest.mark.parametrize("name", ["seeds", "pumps", "surgical", "dyes", "salm", "blocker"])
 def test_ir_published_summaries(mamba, name):
     """Posterior means of the reference's example runs reproduced by 2048 chains of the same run
     (iterations, burnin, thin 2 as printed in the .rst; 2 chains there): |ours - published|
