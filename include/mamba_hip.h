@@ -216,6 +216,11 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
 /* mcmc_worker! loop for all chains of this engine (mcmc.jl:62-83). */
 int mmb_run(mmb_engine* e, const mmb_run_args* args);
 int64_t mmb_iter(const mmb_engine* e);              /* Model.iter after the last window */
+/* Restore Model.iter when resuming from a checkpoint (read(name, ModelChains) followed by
+ * mcmc(mc, iters), fileio.jl:3-11 + mcmc.jl:3-16).  Philox streams are keyed by
+ * (seed, global chain id, iteration), so values + tune + iter + seed reproduce the
+ * uninterrupted trajectory exactly.  Call after mmb_init_chains; iter >= 0. */
+int mmb_set_iter(mmb_engine* e, int64_t iter);
 
 /* ModelState / gettune / settune! (mcmc.jl:56,82; simulation.jl:3-28):
  * values: K x P row-major.  tune: K x mmb_tune_len() doubles in the canonical layout

@@ -10,7 +10,7 @@ The package directory is `mamba.jl_amd/`; import it as `mamba_amd` via
 from . import abi, gelman, ir, model, samplers, summary  # noqa: F401
 from .gelman import gelmandiag, gelmandiag_sharded, psrf_from_sums  # noqa: F401
 from .summary import pool_summary, quantile_sharded, summarystats_sharded  # noqa: F401
-from .mcmc import Chains, Engine, mcmc, mcmc_restart  # noqa: F401
+from .mcmc import Chains, Engine, mcmc, mcmc_restart, read, write  # noqa: F401
 from .model import line, logistic, rats  # noqa: F401
 from .samplers import (AMM, AMWG, HMC, MALA, NUTS, ArgumentError, Gibbs, Multivariate, Sampler,  # noqa: F401
                        Slice, Univariate)

@@ -92,6 +92,7 @@ def _declare(lib):
         "mmb_init_chains": (C.c_int, [P, D, I64, I64, C.c_uint64]),
         "mmb_run": (C.c_int, [P, C.POINTER(RunArgs)]),
         "mmb_iter": (I64, [P]),
+        "mmb_set_iter": (C.c_int, [P, I64]),
         "mmb_get_values": (C.c_int, [P, D]),
         "mmb_set_values": (C.c_int, [P, D]),
         "mmb_tune_len": (I64, [P]),

@@ -591,6 +591,13 @@ int mmb_set_data(mmb_engine* e, const char* name, const double* x, int64_t n) {
 int mmb_num_values(const mmb_engine* e) { return e ? e->P : MMB_E_ARG; }
 int mmb_num_monitored(const mmb_engine* e) { return e ? e->pmon : MMB_E_ARG; }
 int64_t mmb_iter(const mmb_engine* e) { return e ? e->iter : MMB_E_ARG; }
+int mmb_set_iter(mmb_engine* e, int64_t iter) {
+  if (!e) return fail(e, MMB_E_ARG, "null engine");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  if (iter < 0 || iter > 0xffffffffLL) return fail(e, MMB_E_ARG, "iteration out of range");
+  e->iter = iter;
+  return 0;
+}
 int64_t mmb_num_kept(const mmb_engine* e) { return e ? e->n_kept : MMB_E_ARG; }
 
 int64_t mmb_tune_len(const mmb_engine* e) {

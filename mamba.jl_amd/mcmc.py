@@ -55,6 +55,7 @@ class Engine:
         init = np.ascontiguousarray(init, dtype=np.float64)
         self.K = init.shape[0]
         self.chain_offset = int(chain_offset)
+        self.seed = int(seed)
         self._chk(self.lib.mmb_init_chains(self.h, abi.dptr(init), self.K, int(chain_offset),
                                            C.c_uint64(int(seed))))
 
@@ -78,6 +79,9 @@ class Engine:
     @property
     def iter(self):
         return self.lib.mmb_iter(self.h)
+
+    def set_iter(self, it):
+        self._chk(self.lib.mmb_set_iter(self.h, int(it)))
 
     def values(self):
         v = np.empty((self.K, self.P))
@@ -236,3 +240,51 @@ def mcmc_restart(mc, iters, verbose=False):
     model.iter = eng.iter
     value = np.concatenate([mc.value, draws], axis=0) if draws is not None else mc.value
     return Chains(value, mc.names, mc.start, mc.thin, mc.chains, model, eng)
+
+
+_CKPT_KIND = "mamba_amd.ModelChains/1"
+
+
+def write(name, c):
+    """write(name, c::AbstractChains) (fileio.jl:10-12): save the chains and, for a
+    ModelChains with a live engine, the resumable model state (ModelState values + tune,
+    Model.iter, Philox seed, global chain offset, Model.burnin).  The file is a plain
+    .npz (no pickled objects): `read(name, model=...)` restores an engine on any device
+    and `mcmc_restart` then continues exactly where the writer stopped."""
+    arrays = dict(kind=np.array(_CKPT_KIND), value=np.asarray(c.value, dtype=np.float64),
+                  names=np.array(c.names, dtype=np.str_), start=np.int64(c.start),
+                  thin=np.int64(c.thin), chains=np.asarray(c.chains, dtype=np.int64))
+    eng = c.engine
+    if eng is not None and getattr(eng, "h", None) is not None and eng.K > 0:
+        arrays.update(values=eng.values(), tune=eng.tune(), iter=np.int64(eng.iter),
+                      seed=np.uint64(eng.seed), chain_offset=np.int64(eng.chain_offset),
+                      model_burnin=np.int64(getattr(c.model, "burnin", 0)))
+    with open(name, "wb") as f:  # np.savez would append ".npz" to a bare name
+        np.savez(f, **arrays)
+
+
+def read(name, model=None, device=0):
+    """read(name, ModelChains) (fileio.jl:3-8): load chains written by `write`.  With
+    `model` (the same Model, inputs set, as the writer's: closures are not serialised),
+    the saved state is restored into a new engine on `device`, ready for
+    `mcmc_restart(mc, iters)`.  Raises TypeError if the file holds no chains."""
+    with np.load(name, allow_pickle=False) as z:
+        if "kind" not in z.files or str(z["kind"]) != _CKPT_KIND:
+            raise TypeError(f'read("{name}", ModelChains): not a chains file')
+        d = {k: z[k] for k in z.files}
+    eng = None
+    if model is not None:
+        if "values" not in d:
+            raise ArgumentError("file holds no model state to resume from")
+        vals = d["values"]
+        eng = Engine(model, device)
+        if vals.shape[1] != eng.P:
+            eng.close()
+            raise ArgumentError(f"saved state has {vals.shape[1]} values per chain, model has {eng.P}")
+        eng.init_chains(vals, chain_offset=int(d["chain_offset"]), seed=int(d["seed"]))
+        eng.set_tune(d["tune"])
+        eng.set_iter(int(d["iter"]))
+        model.burnin = int(d["model_burnin"])
+        model.iter = int(d["iter"])
+    return Chains(d["value"], [str(x) for x in d["names"]], int(d["start"]), int(d["thin"]),
+                  d["chains"], model, eng)

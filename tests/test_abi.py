@@ -96,3 +96,22 @@ def test_python_argument_errors(mamba):
                    burnin=10)
     with pytest.raises(mamba.ArgumentError, match="fewer initial values"):
         m.setinputs(mamba.model.RATS_DATA).init_matrix(mamba.model.RATS_INITS, 3)
+
+
+def test_chains_file_round_trip(mamba, tmp_path):
+    """write/read (fileio.jl:3-12) of chains without engine state: plain .npz, no pickle."""
+    val = np.random.default_rng(0).normal(size=(7, 3, 4))
+    c = mamba.Chains(val, ["s2_c", "mu_beta", "alpha0"], 1002, 2, np.arange(1, 5))
+    p = str(tmp_path / "sim.chains")
+    mamba.write(p, c)
+    r = mamba.read(p)
+    np.testing.assert_array_equal(r.value, val)
+    assert r.names == c.names and r.start == 1002 and r.thin == 2
+    assert list(r.range) == list(c.range)
+    np.testing.assert_array_equal(r.chains, c.chains)
+    with pytest.raises(mamba.ArgumentError):  # no model state saved
+        mamba.read(p, model=mamba.rats())
+    bad = str(tmp_path / "bad.npz")
+    np.savez(bad, value=val)
+    with pytest.raises(TypeError):
+        mamba.read(bad)

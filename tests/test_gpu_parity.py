@@ -239,3 +239,82 @@ def test_device_summary_logistic_many_params(mamba):
     got = mamba.summarystats_sharded(eng, batch_size=50)
     np.testing.assert_allclose(got[:, :4], sr.summarystats(d, 50)[:, :4], rtol=1e-9)
     np.testing.assert_array_equal(mamba.quantile_sharded(eng, (0.1, 0.5, 0.9)), sr.quantile(d, (0.1, 0.5, 0.9)))
+
+
+@pytest.mark.parametrize("scheme", ["gibbs_amm", "reference"])
+def test_checkpoint_file_resume(mamba, tmp_path, scheme):
+    """write(name, mc) + read(name, ModelChains) + mcmc(mc, iters) (fileio.jl:3-12,
+    mcmc.jl:3-16): a run checkpointed to a file and resumed in a fresh engine equals the
+    uninterrupted run draw for draw (values, AMM moments/factors, AMWG/Slice tune, iter)."""
+    sch = {"gibbs_amm": mamba.model.rats_scheme_gibbs_amm,
+           "reference": mamba.model.rats_scheme_reference}[scheme]
+    init = mamba.model.rats_init_ls(96, seed=4)
+    m = rats(mamba, sch())
+    e = mamba.Engine(m)
+    e.init_chains(init, chain_offset=32, seed=11)
+    full = e.run(70, burnin=20, thin=2)
+    m1 = rats(mamba, sch())
+    e1 = mamba.Engine(m1)
+    e1.init_chains(init, chain_offset=32, seed=11)
+    a = e1.run(30, burnin=20, thin=2)
+    m1.iter, m1.burnin = e1.iter, 20
+    mc = mamba.Chains(a, m1.monitor_names, 22, 2, np.arange(33, 129), m1, e1)
+    p = str(tmp_path / "rats.chains")
+    mamba.write(p, mc)
+    e1.close()
+    m2 = rats(mamba, sch())
+    mc2 = mamba.read(p, model=m2)
+    assert mc2.engine.iter == 30
+    mc3 = mamba.mcmc_restart(mc2, 40)
+    np.testing.assert_array_equal(mc3.value, full)
+    assert list(mc3.range) == list(range(22, 71, 2))
+
+
+@pytest.mark.parametrize("name", ["nuts_slice", "amwg", "hmc", "mala_sigma_gibbs"])
+def test_checkpoint_file_resume_line(mamba, tmp_path, name):
+    """Checkpoint inside NUTS's dual-averaging burnin (model burnin 150, written at 100):
+    the NUTS tune (eps, epsbar, Hbar, mu, m, init flag) and Model.burnin travel in the file."""
+    init = mamba.model.line_init_matrix(256, seed=4)
+    e = mamba.Engine(line(mamba, LINE_SCHEMES[name](mamba)))
+    e.init_chains(init, seed=8)
+    full = e.run(300, burnin=150, thin=2, model_burnin=150)
+    m1 = line(mamba, LINE_SCHEMES[name](mamba))
+    e1 = mamba.Engine(m1)
+    e1.init_chains(init, seed=8)
+    a = e1.run(100, burnin=150, thin=2, model_burnin=150)
+    assert a is None
+    m1.iter, m1.burnin = e1.iter, 150
+    mc = mamba.Chains(np.empty((0, e1.pmon, 256)), m1.monitor_names, 152, 2, np.arange(1, 257), m1, e1)
+    p = str(tmp_path / "line.chains")
+    mamba.write(p, mc)
+    e1.close()
+    mc2 = mamba.read(p, model=line(mamba, LINE_SCHEMES[name](mamba)))
+    assert mc2.model.burnin == 150 and mc2.engine.iter == 100
+    b = mc2.engine.run(200, burnin=150, thin=2, model_burnin=mc2.model.burnin)
+    np.testing.assert_array_equal(b, full)
+
+
+@pytest.mark.parametrize("name", ["nuts", "hmc"])
+def test_checkpoint_file_resume_logistic(mamba, tmp_path, name):
+    """Logistic (config 4 at N=1000): the resumable NUTS / HMC machines hold no state across
+    iteration boundaries beyond values + tune, so a file checkpoint resumes exactly."""
+    sch = (lambda: [mamba.NUTS("beta")]) if name == "nuts" else (lambda: LOGISTIC_GRAD_SCHEMES["hmc"](mamba, 50))
+    K = 100
+    init = np.random.default_rng(8).normal(0.0, 0.1, (K, 50))
+    m, _ = logistic(mamba, 1000, 50, sch())
+    e = mamba.Engine(m)
+    e.init_chains(init, seed=3)
+    full = e.run(30, burnin=10, thin=1, model_burnin=15)
+    m1, _ = logistic(mamba, 1000, 50, sch())
+    e1 = mamba.Engine(m1)
+    e1.init_chains(init, seed=3)
+    a = e1.run(12, burnin=10, thin=1, model_burnin=15)
+    m1.iter, m1.burnin = e1.iter, 15
+    mc = mamba.Chains(a, m1.monitor_names, 11, 1, np.arange(1, K + 1), m1, e1)
+    p = str(tmp_path / "lg.chains")
+    mamba.write(p, mc)
+    e1.close()
+    m2, _ = logistic(mamba, 1000, 50, sch())
+    mc2 = mamba.read(p, model=m2)
+    b = mc2.engine.run(18, burnin=10, thin=1, model_burnin=mc2.model.burnin)
+    np.testing.assert_array_equal(np.concatenate([mc2.value, b]), full)
