@@ -318,3 +318,48 @@ def test_checkpoint_file_resume_logistic(mamba, tmp_path, name):
     mc2 = mamba.read(p, model=m2)
     b = mc2.engine.run(18, burnin=10, thin=1, model_burnin=mc2.model.burnin)
     np.testing.assert_array_equal(np.concatenate([mc2.value, b]), full)
+
+
+@pytest.mark.parametrize("K,iters,burnin,thin,offset", [(1, 13, 3, 3, 0), (37, 21, 0, 1, 1000), (129, 17, 16, 1, 7), (64, 14, 4, 5, 0)])
+def test_rats_ragged_shapes(mamba, oracle, K, iters, burnin, thin, offset):
+    """Chain counts that fill neither a wave (2 chains) nor a workgroup (8 chains), windows
+    that are not a multiple of the kernel's iterations per launch, a single kept draw,
+    and nonzero global chain offsets."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_ls(K, seed=6)
+    eng, dg, st, do = both(mamba, oracle, m, init, iters, burnin, thin, offset=offset)
+    assert dg.shape == do.shape == ((iters - burnin) // thin, 3, K)
+    np.testing.assert_allclose(dg, do, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(eng.values(), st["values"], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("K", [1, 65])
+@pytest.mark.parametrize("name", ["amm", "nuts_slice"])
+def test_line_ragged_shapes(mamba, oracle, name, K):
+    m = line(mamba, LINE_SCHEMES[name](mamba))
+    init = mamba.model.line_init_matrix(K, seed=5)
+    eng, dg, st, do = both(mamba, oracle, m, init, 71, 10, 3, offset=3, model_burnin=20)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+
+
+def test_empty_window_leaves_state(mamba):
+    """iters = 0: no kernel work, no draws, Model.iter and the chain state unchanged."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(40, seed=1), seed=3)
+    eng.run(9, burnin=0, thin=1)
+    v, t = eng.values(), eng.tune()
+    assert eng.run(0, burnin=0, thin=1) is None
+    assert eng.iter == 9
+    np.testing.assert_array_equal(eng.values(), v)
+    np.testing.assert_array_equal(eng.tune(), t)
+
+
+def test_logistic_single_chain(mamba, oracle):
+    """K = 1: one live lane of the first 16-chain MFMA tile, 63 padded chains."""
+    m, _ = logistic(mamba, 1000, 50)
+    init = np.random.default_rng(1).normal(0.0, 0.1, (1, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 12, 4, 2, model_burnin=6)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
