@@ -84,7 +84,10 @@ struct Mdl<MMB_MODEL_IR> {
           v = vals[arg + (int)A.ir_pool[ir_const_ref(A.ir_code, pc) + i]];
         } else if (op == MMB_IR_OP_DATA) v = A.ir_pool[arg + i];
         else v = A.ir_pool[arg];  // MMB_IR_OP_DATAS
-        stk[sp * G + lane] = acc;
+        // the bottom slot is never popped: no spill for an expression's first leaf (seeds
+        // 1.04e7 -> 1.095e7 /s; folding a leaf into a following binary op instead of the
+        // spill / reload measured slower, 1.025e7: the extra code-word load costs more)
+        if (sp > 0) stk[sp * G + lane] = acc;
         ++sp;
         acc = v;
       } else if (op < 32) {
