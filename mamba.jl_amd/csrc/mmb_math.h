@@ -347,8 +347,8 @@ MMB_HD double mmb_exp_neg(double x) {
 
 /* log1p(t) for t in [0, 1]: 2 atanh(s), s = t / (2 + t) <= 1/3, as the odd series
  * 2 s sum_k s^(2k) / (2k + 1) to k = 16 (truncation < 2^-56); one division, no branches. */
-MMB_HD double mmb_log1p_unit(double t) {
-  const double s = t / (2.0 + t);
+/* 2 atanh(s) = log((1 + s) / (1 - s)) for 0 <= s <= 1/3: the odd series to s^33 in Horner form */
+MMB_HD double mmb_atanh2_series(double s) {
   const double z = s * s;
   double p = 1.0 / 33.0;
   p = fma(p, z, 1.0 / 31.0);
@@ -369,14 +369,17 @@ MMB_HD double mmb_log1p_unit(double t) {
   const double s2 = 2.0 * s;
   return fma(s2, z * p, s2);
 }
+MMB_HD double mmb_log1p_unit(double t) { return mmb_atanh2_series(t / (2.0 + t)); }
 
-/* Per observation of the logistic model: lp = y eta - softplus(eta), res = y - invlogit(eta),
- * both from t = exp(-|eta|) (stable for any eta). */
 MMB_HD void mmb_logistic_terms(double eta, double y, double* lp, double* res) {
-  double t = mmb_exp_neg(-fabs(eta));
-  double sp = (eta > 0.0 ? eta : 0.0) + mmb_log1p_unit(t);
+  /* one IEEE division shared by both quotients: R = 1/((1+t)(2+t)), 1/(1+t) = (2+t) R,
+   * t/(2+t) = t (1+t) R (a few ulp instead of correctly rounded; host and device agree) */
+  const double t = mmb_exp_neg(-fabs(eta));
+  const double a = 1.0 + t, b = 2.0 + t;
+  const double R = 1.0 / (a * b);
+  const double sp = (eta > 0.0 ? eta : 0.0) + mmb_atanh2_series((t * a) * R);
   *lp = y * eta - sp;
-  double q = 1.0 / (1.0 + t);
+  const double q = b * R;
   *res = y - (eta >= 0.0 ? q : t * q);
 }
 

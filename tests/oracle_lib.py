@@ -41,6 +41,7 @@ class Oracle:
             getattr(L, f).restype = C.c_double
             getattr(L, f).argtypes = [C.c_double]
         L.orc_sincos2pi.argtypes = [C.c_double, D, D]
+        L.orc_logistic_terms.argtypes = [C.c_double, C.c_double, D, D]
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32)] * 3
         for f in ("orc_uniform", "orc_normal"):
             getattr(L, f).restype = C.c_double

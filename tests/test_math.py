@@ -92,3 +92,30 @@ def test_gamma_marsaglia_tsang(oracle, a):
     se = np.sqrt(a / 20000)
     assert abs(g.mean() - a) < 5 * se
     assert abs(g.var() / a - 1) < 0.06
+
+
+def test_logistic_terms_accuracy(oracle):
+    """mmb_logistic_terms (config-4 per-row terms, one shared division): lp = y*eta -
+    softplus(eta) and res = y - invlogit(eta) against an 80-bit long-double evaluation."""
+    import ctypes as C
+    r = np.random.default_rng(11)
+    eta = np.concatenate([r.normal(0, 3, 20000), r.uniform(-745, 745, 2000), [0.0, -0.0, 1e-300, -1e-300, 40.0, -40.0]])
+    lp1, rs1, lp0, rs0 = (np.empty(eta.size) for _ in range(4))
+    a, b = C.c_double(), C.c_double()
+    for k, e in enumerate(eta):
+        oracle.L.orc_logistic_terms(float(e), 1.0, C.byref(a), C.byref(b))
+        lp1[k], rs1[k] = a.value, b.value
+        oracle.L.orc_logistic_terms(float(e), 0.0, C.byref(a), C.byref(b))
+        lp0[k], rs0[k] = a.value, b.value
+    E = eta.astype(np.longdouble)
+    t = np.exp(-np.abs(E))
+    sp = np.maximum(E, 0) + np.log1p(t)
+    sig = np.where(E >= 0, 1 / (1 + t), t / (1 + t))
+    for got, ref in ((lp1, E - sp), (lp0, -sp)):
+        ref = ref.astype(np.float64)
+        # y*eta - softplus(eta) cancels for large |eta|: scale by max(|lp|, |eta|) (measured 5.1e-16 * scale)
+        scale = np.maximum(np.maximum(np.abs(ref), np.abs(eta)), 1e-300)
+        assert (np.abs(got - ref) / scale).max() <= 8e-16
+    # residuals: absolute error (they are the score terms summed into the gradient)
+    assert np.abs(rs1 - (1 - sig).astype(np.float64)).max() <= 4.5e-16
+    assert np.abs(rs0 - (-sig).astype(np.float64)).max() <= 4.5e-16
