@@ -9,6 +9,13 @@ N=8).  A step = one sample!(m) sweep of every chain (one mcmc_worker! iteration)
 the keep rule and the Chains write (thin 2, draws kept in HBM).  Steps run as one
 mmb_run window (kernels of 8 iterations); state and data are resident in HBM.
 
+Steady state: before --warmup, an untimed adaptation pre-run (--adapt-prerun, default
+128 >= 2d+2 = 62 for the 30-d AMM blocks) takes every chain past AMM's switch to the
+adaptive proposal (tune.m > 2n, amm.jl:73-75), so the timed steps run the configuration
+they name: mixture proposal + full-rank pivoted Cholesky (amm.jl:72-90) every update.
+The timed window's own kernel time (HIP events on the engine stream) is checked against
+its wall time: the run fails if kernel ms per step exceeds ms_per_step by > 5 %.
+
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
 
@@ -33,6 +40,7 @@ sys.path.insert(0, ROOT)
 CHAINS_PER_GPU = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (spec, dense)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_rats_hbm_traffic.json")
 
 
 def parse():
@@ -40,11 +48,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
+    p.add_argument("--adapt-prerun", type=int, default=None,
+                   help="untimed iterations before --warmup (default 128; logistic 0)")
     p.add_argument("--chains", type=int, default=None, help="chains per GPU")
     p.add_argument("--workload", default="rats", choices=["rats", "line_amm", "logistic", "seeds_ir", "rats_ir"])
     p.add_argument("--thin", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--scheme", default="gibbs_amm",
                    help="gibbs_amm (metric config) | reference | ablations: amm_noadapt, gibbs_only")
     a = p.parse_args()
@@ -54,37 +64,91 @@ def parse():
     a.chains = a.chains or k
     a.steps = a.steps if a.steps is not None else st
     a.warmup = a.warmup if a.warmup is not None else wu
+    if a.adapt_prerun is None:
+        a.adapt_prerun = 0 if a.workload == "logistic" else 128
     return a
 
 
-def cpu_baseline(mb, model, init, seconds, what="rats Gibbs+AMM sweep", per_thread=64, warm=64,
-                 model_burnin=None):
-    """The CPU oracle (same algorithm, same Philox streams) on the host cores: bounded
-    sample (a few thousand chain-updates per thread), OpenMP over chains."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
-    orc = oracle_lib.Oracle()
-    threads = min(os.cpu_count() or 1, 16)
-    K = min(per_thread * threads, init.shape[0])
-    st = orc.new_state(model, init[:K])
-    orc.run(model, st, warm, seed=7, nthreads=threads, draws=False, model_burnin=model_burnin)  # warm-up
-    iters, t = 16, 0.0
-    while True:
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota (on the
+    GPU box os.cpu_count() is the whole machine while the job's share is a quota)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, {"nproc": nproc, "affinity": aff, "cgroup_quota": quota}
+
+
+def _timed_runs(orc, model, st, iters, threads, runs, model_burnin):
+    ts = []
+    for _ in range(runs):
         t0 = time.perf_counter()
         orc.run(model, st, iters, burnin=0, thin=2, seed=7, nthreads=threads, draws=True,
                 model_burnin=model_burnin)
-        t = time.perf_counter() - t0
-        if t > seconds / 2 or iters >= 8192:
-            break
-        iters *= 2
-    return {"value": K * iters / t, "unit": "chain-updates/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/oracle.c, {K} chains x {iters} iterations (after {warm} warm-up) of the same "
-                      f"{what}, OpenMP {threads} threads, {t:.1f} s"}
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2], ts
+
+
+def _oracle_rate(orc, model, init, threads, per_thread, warm, run_s, runs, model_burnin):
+    """Median-of-`runs` chain-updates/s of the oracle on `threads` OpenMP threads, timed
+    after `warm` untimed iterations (AMM past its m > 2d switch, amm.jl:73-75)."""
+    K = min(per_thread * threads, init.shape[0])
+    st = orc.new_state(model, init[:K])
+    orc.run(model, st, warm, seed=7, nthreads=threads, draws=False, model_burnin=model_burnin)
+    iters = 4
+    t, _ = _timed_runs(orc, model, st, iters, threads, 1, model_burnin)     # calibration
+    iters = int(min(8192, max(4, iters * run_s / max(t, 1e-6))))
+    med, ts = _timed_runs(orc, model, st, iters, threads, runs, model_burnin)
+    return K * iters / med, K, iters, [round(x, 3) for x in ts]
+
+
+def cpu_baseline(model, init, seconds, what="rats Gibbs+AMM sweep", per_thread=64, warm=128,
+                 model_burnin=None, extra=None):
+    """The CPU oracle (same algorithm, same Philox streams; the Julia reference cannot run
+    here) on the host cores, SURVEY §8(d): all usable cores and 1 thread, median of 5 runs
+    each, bounded to about `seconds` of wall time.  `extra`: (label, model, init) timed
+    beside it on all cores (rats: the reference Slice+AMWG scheme)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    orc = oracle_lib.Oracle()
+    threads, host = host_cores()
+    share = seconds / (10.0 + (3.0 if extra else 0.0))  # 5 all-core + 5 one-thread (+3 extra) runs
+    v, K, iters, ts = _oracle_rate(orc, model, init, threads, per_thread, warm, share, 5, model_burnin)
+    v1, K1, it1, ts1 = _oracle_rate(orc, model, init, 1, per_thread, warm, share, 5, model_burnin)
+    out = {"value": v, "unit": "chain-updates/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/oracle.c (CPU restatement; the Julia reference cannot run here): {K} chains x "
+                     f"{iters} iterations of the same {what} after {warm} untimed warm-up iterations, "
+                     f"OpenMP {threads} threads, median of 5 runs",
+           "runs_s": ts, "single_thread": {"value": v1, "chains": K1, "iters": it1, "runs_s": ts1},
+           "host": host}
+    if extra:
+        label, m2, init2 = extra
+        v2, K2, it2, ts2 = _oracle_rate(orc, m2, init2, threads, per_thread, warm, share, 3, model_burnin)
+        out[label] = {"value": v2, "cores": threads, "chains": K2, "iters": it2, "runs_s": ts2}
+    return out
 
 
 def scheme_for(mb, name):
+    """Named rats schemes; "gibbs_amm:beta=0.5,adapt=burnin" overrides AMM keywords."""
     import numpy as np
     G = mb.Gibbs
+    if name.startswith("gibbs_amm:"):
+        kw = dict(x.split("=") for x in name.split(":", 1)[1].split(","))
+        beta = float(kw.get("beta", 0.05))
+        adapt = kw.get("adapt", "all")
+        sa, sb = float(kw.get("sa", 1.0)), float(kw.get("sb", 0.01))
+        return [G("s2_c"), mb.AMM("alpha", sa * np.eye(30), adapt=adapt, beta=beta), G("mu_alpha"),
+                G("s2_alpha"), mb.AMM("beta", sb * np.eye(30), adapt=adapt, beta=beta), G("mu_beta"),
+                G("s2_beta")]
     if name == "gibbs_amm":
         return mb.model.rats_scheme_gibbs_amm()
     if name == "reference":
@@ -97,14 +161,19 @@ def scheme_for(mb, name):
     raise SystemExit(f"unknown scheme {name}")
 
 
+def rats_model(mb, scheme):
+    model = mb.rats()
+    model.setinputs(mb.model.RATS_DATA)
+    model.setsamplers(scheme)
+    return model
+
+
 def setup_workload(mb, args, rank):
     """Model, scheme, per-chain inits and the run keywords of one BASELINE config."""
     import numpy as np
     K = args.chains
     if args.workload == "rats":
-        model = mb.rats()
-        model.setinputs(mb.model.RATS_DATA)
-        model.setsamplers(scheme_for(mb, args.scheme))
+        model = rats_model(mb, scheme_for(mb, args.scheme))
         init = mb.model.rats_init_ls(K, seed=1000 + rank)
         desc = ("rats mixed Gibbs+AMM sweep (BASELINE configs[2]; configs[4] at N=8)"
                 if args.scheme == "gibbs_amm" else f"rats scheme {args.scheme}")
@@ -136,6 +205,21 @@ def setup_workload(mb, args, rank):
     model.setsamplers([mb.NUTS("beta")])
     init = np.random.default_rng(1000 + rank).normal(0.0, 0.1, (K, 50))
     return model, init, "logistic N=10000 p=50 NUTS (BASELINE configs[3])", {"thin": 1}, "f64"
+
+
+def pmc_traffic(args, W):
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC pass of this exact
+    kernel configuration (profiles/, gathered and corrected by tools/hbm_traffic.py as
+    MI355X_MICROARCH.md prescribes); None when no such pass matches."""
+    if args.workload != "rats" or not os.path.exists(TRAFFIC_FILE):
+        return None, None
+    try:
+        t = json.load(open(TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    if (t.get("scheme"), t.get("chains"), t.get("iters_per_launch")) != (args.scheme, args.chains, W):
+        return None, None
+    return t.get("bytes_per_launch"), os.path.relpath(TRAFFIC_FILE, ROOT)
 
 
 def main():
@@ -173,22 +257,38 @@ def main():
         torch.cuda.synchronize()
         eng.sync()
 
-    # warmup: adaptation reaches steady state (AMM m > 2d uses the adaptive factor; NUTS
-    # dual averaging runs while iter <= model_burnin = warmup, then the step size is fixed)
-    mburn = args.warmup if nuts else 0
+    # untimed adaptation pre-run, then warmup: AMM's m > 2d switch has happened in every chain
+    # before the timed window; NUTS dual averaging runs while iter <= model_burnin (the warmup),
+    # then the step size is fixed (nuts.jl:52)
+    pre = args.adapt_prerun
+    mburn = pre + args.warmup if nuts else 0
+    if pre > 0:
+        eng.run(pre, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False)
     eng.run(args.warmup, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False)
+    nuts_before = eng.nuts_stats() if nuts else None
     barrier()
     t0 = time.perf_counter()
-    eng.run(args.steps, burnin=args.warmup, thin=thin, model_burnin=mburn, draws=False, keep_device=True)
+    eng.run(args.steps, burnin=pre + args.warmup, thin=thin, model_burnin=mburn, draws=False, keep_device=True,
+            time_kernels=True)
     barrier()
     dt = time.perf_counter() - t0
+    t_kms, t_launches, t_units = eng.kernel_time()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     total_units = K * world * args.steps
     value = total_units / dt
+    ms_per_step = dt / args.steps * 1e3
+    kernel_ms_per_step = t_kms / args.steps
+    if kernel_ms_per_step > 1.05 * ms_per_step:
+        raise SystemExit(f"bench: kernel time per step {kernel_ms_per_step:.4f} ms exceeds the timed "
+                         f"window's {ms_per_step:.4f} ms by more than 5 % — timing is inconsistent")
     grads_timed = eng.grad_evals() if nuts else 0
+    nuts_timed = None
+    if nuts:
+        after = eng.nuts_stats()
+        nuts_timed = {k: after[k] - nuts_before[k] for k in after}
 
     psrf = None
     # Gelman-Rubin over all chains of all GPUs: device partials + one RCCL all-reduce
@@ -209,7 +309,8 @@ def main():
 
     psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax)
 
-    # roofline of the dominant kernel; per-launch device time from HIP events on the engine's stream
+    # roofline of the dominant kernel; per-launch device time from HIP events on the engine's
+    # stream, over full launches in the same steady state as the timed window
     if nuts:  # lg_grad_kernel: 4*N*p algorithmic flops per gradient (X*beta and X'*res)
         nroof = 16
         eng.run(nroof, burnin=0, thin=1, model_burnin=mburn, draws=False, time_kernels=True)
@@ -224,24 +325,22 @@ def main():
     else:
         W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
                                "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "64"))
-        nroof = max(W * 8, 64)
+        nroof = max(W * 16, 64)
         eng.run(nroof, burnin=0, thin=thin, model_burnin=0, draws=False, keep_device=False, time_kernels=True)
         kms, launches, units = eng.kernel_time()
         per_update = eng.state_bytes() + 8.0 * eng.pmon / thin  # 2*S_state + S_draw/thin
         bytes_per_launch = per_update * units / launches
         avg_ms = kms / launches
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
-        if args.workload == "rats" and args.scheme == "gibbs_amm" and os.path.exists(tfile):
-            try:
-                traffic = json.load(open(tfile)).get("bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic, tsrc = pmc_traffic(args, W)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "sweep_kernel",
-                "algorithmic_bytes_per_chain_update": per_update,
-                "avg_launch_ms": avg_ms, "chain_updates_per_launch": units / launches}
+                "algorithmic_bytes_per_chain_update": per_update, "algorithmic_bytes_per_launch": bytes_per_launch,
+                "avg_launch_ms": avg_ms, "launches": launches, "chain_updates_per_launch": units / launches}
+        if tsrc:
+            roof["traffic_source"] = tsrc
+    roof["timed_window_kernel_ms_per_step"] = kernel_ms_per_step
+    roof["timed_window_launches"] = t_launches
 
     out = {
         "metric": "chain-updates/sec (iters×chains) on rats model at 1/2/4/8 MI355X",
@@ -250,7 +349,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
+        "adapt_prerun": pre,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -270,19 +370,23 @@ def main():
     if args.workload == "rats":
         out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8")),
                               "amm_adapt": "all"})
+    if nuts_timed is not None:
+        out["nuts"] = nuts_timed
     if psrf is not None:
         out["gelman_rubin_psrf"] = [float(x) for x in psrf[:, 0]]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if args.workload == "rats":
-            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds)
+            ref = rats_model(mb, scheme_for(mb, "reference"))
+            out["cpu_baseline"] = cpu_baseline(model, init_all, args.cpu_seconds,
+                                               extra=("reference_scheme", ref, init_all))
         elif args.workload == "line_amm":
-            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds, "line AMM update",
-                                               per_thread=256, warm=64)
+            out["cpu_baseline"] = cpu_baseline(model, init_all, args.cpu_seconds, "line AMM update",
+                                               per_thread=256)
         elif args.workload.endswith("_ir"):
-            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds,
+            out["cpu_baseline"] = cpu_baseline(model, init_all, args.cpu_seconds,
                                                f"{args.workload} node-IR sweep", per_thread=16, warm=16)
         else:
-            out["cpu_baseline"] = cpu_baseline(mb, model, init_all, args.cpu_seconds, "logistic NUTS update",
+            out["cpu_baseline"] = cpu_baseline(model, init_all, args.cpu_seconds, "logistic NUTS update",
                                                per_thread=4, warm=20, model_burnin=20)
     if rank == 0:
         print(json.dumps(out))

@@ -65,7 +65,7 @@ typedef enum {
   MMB_SAMPLER_NUTS = 3,  /* src/samplers/nuts.jl:47-56 */
   MMB_SAMPLER_SLICE = 4, /* src/samplers/slice.jl:47-58 */
   MMB_SAMPLER_GIBBS = 5, /* user Sampler(params, f): conjugate full conditional of the block's node,
-                            e.g. doc/tutorial/line.jl:168-186 */
+                            e.g. doc/tutorial/line.jl:27-45 */
   MMB_SAMPLER_HMC = 6,   /* src/samplers/hmc.jl:47-65 */
   MMB_SAMPLER_MALA = 7   /* src/samplers/mala.jl:43-58 */
 } mmb_sampler_kind;
@@ -273,6 +273,11 @@ int mmb_state_bytes(const mmb_engine* e, double* bytes_per_chain_update);
 /* Gradient evaluations (logpdf!+gradlogpdf! calls, sampler.jl:97-119) in the last mmb_run,
  * summed over chains; counted on device by the batched-gradient (logistic) engine, 0 else. */
 int mmb_grad_evals(mmb_engine* e, int64_t* n);
+/* NUTS tree statistics since mmb_init_chains, all NUTS blocks and chains: out[0] = completed
+ * updates, out[1] = updates stopped by the depth cap MMB_NUTS_MAX_DEPTH (16) while the
+ * reference's unbounded doubling loop (nuts.jl:106-125) would have continued, out[2] = sum of
+ * final tree depths j.  out[1] == 0 means the cap never changed a draw. */
+int mmb_nuts_stats(mmb_engine* e, int64_t out[3]);
 
 #ifdef __cplusplus
 }

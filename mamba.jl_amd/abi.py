@@ -109,6 +109,7 @@ def _declare(lib):
         "mmb_kernel_time": (C.c_int, [P, D, C.POINTER(I64), C.POINTER(I64)]),
         "mmb_state_bytes": (C.c_int, [P, D]),
         "mmb_grad_evals": (C.c_int, [P, C.POINTER(I64)]),
+        "mmb_nuts_stats": (C.c_int, [P, C.POINTER(I64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

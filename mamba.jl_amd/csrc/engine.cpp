@@ -76,6 +76,7 @@ struct mmb_engine {
   int64_t* lg_itc = nullptr;
   int64_t lg_steps = 0;  // gradient steps of the last window
   unsigned long long* lg_ngrad = nullptr;
+  unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum} since init_chains
   // draws of the last window
   double* d_draws = nullptr;
   size_t draws_cap = 0;
@@ -495,6 +496,8 @@ static void free_dev(mmb_engine* e) {
     e->lg_itc = nullptr;
     if (e->lg_ngrad) (void)hipFree(e->lg_ngrad);
     e->lg_ngrad = nullptr;
+    if (e->d_nstat) (void)hipFree(e->d_nstat);
+    e->d_nstat = nullptr;
   }
   if (e->d_draws) (void)hipFree(e->d_draws);
   e->d_vals = nullptr;
@@ -714,6 +717,8 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
   e->iter = 0;
   e->n_kept = 0;
   HIPCHK(e, dalloc(&e->d_vals, (size_t)K * e->VS));
+  HIPCHK(e, dalloc(&e->d_nstat, 3));
+  HIPCHK(e, hipMemset(e->d_nstat, 0, 3 * sizeof(unsigned long long)));
   const size_t DP = e->DP, TP = e->TP;
   for (auto& h : e->blocks) {
     HIPCHK(e, dalloc(&h.m, K));
@@ -797,6 +802,7 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.seed = e->seed;
   A.nb = (int32_t)e->blocks.size();
   A.vals = e->d_vals;
+  A.nuts_stat = e->d_nstat;
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
   if (e->model == MMB_MODEL_IR) {
@@ -863,6 +869,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.draws = draws;
   A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count;
   A.ngrad = e->lg_ngrad;
+  A.nstat = e->d_nstat;
   HIPCHK(e, hipMemsetAsync(e->lg_ngrad, 0, sizeof(unsigned long long), e->stream));
   e->kernel_ms = 0.0;
   e->launches = 0;
@@ -1284,6 +1291,18 @@ int mmb_state_bytes(const mmb_engine* e, double* bytes) {
   return 0;
 }
 
+
+int mmb_nuts_stats(mmb_engine* e, int64_t* out) {
+  if (!e || !out) return fail(e, MMB_E_ARG, "null argument");
+  unsigned long long v[3] = {0, 0, 0};
+  if (e->d_nstat) {
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpyAsync(v, e->d_nstat, sizeof v, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  for (int i = 0; i < 3; ++i) out[i] = (int64_t)v[i];
+  return 0;
+}
 
 int mmb_grad_evals(mmb_engine* e, int64_t* n) {
   if (!e || !n) return fail(e, MMB_E_ARG, "null argument");

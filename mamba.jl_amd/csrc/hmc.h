@@ -1,4 +1,4 @@
-// hmc.h — HMC (src/samplers/hmc.jl:72-111) and MALA (src/samplers/mala.jl:67-90) as
+// hmc.h — HMC (src/samplers/hmc.jl:72-111) and MALA (src/samplers/mala.jl:67-86) as
 // resumable machines, the same contract as nuts.h: advance() runs until it needs logf/grad
 // at S.x (returns true; the caller fills S.lf and S.g and calls again) or the update is
 // complete (returns false).  Line calls the model gradient inline; the logistic engine
@@ -209,7 +209,7 @@ struct Hmc {
     return -0.5 * dot(g, w, E.d);
   }
 
-  // sample!(v::MALAVariate, logfgrad) (mala.jl:67-90)
+  // sample!(v::MALAVariate, logfgrad) (mala.jl:67-86)
   __device__ static bool advance_mala(St& S, const Env& E, const Grp<G>& g) {
     const double s = sqrt(E.eps);
     switch (S.pc) {

@@ -43,4 +43,5 @@ struct LgArgs {
   double* lpart;           // [MMB_LG_NG][K]
   int32_t* count;          // [2] requests in the current step (ping-pong by step parity)
   unsigned long long* ngrad;  // total gradient evaluations of the window
+  unsigned long long* nstat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat)
 };

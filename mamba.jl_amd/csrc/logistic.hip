@@ -105,6 +105,7 @@ struct LgNuts {
     E.ru = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_UNIFORM);
     E.ri = mmb_rng_make(A.seed, chain, (uint32_t)cur, 0u, MMB_SUB_INIT);
     E.F = A.frames + (size_t)c * LgFr::DBL;
+    E.stat = A.nstat;
     return NU::advance(S, E, g);
   }
 };

@@ -6,7 +6,7 @@
  * Why shared: Mamba.jl's MersenneTwister/ziggurat streams and openlibm cannot
  * be reproduced, so parity is oracle <-> GPU on identical Philox streams
  * (SURVEY §8c).  Bit-exact accept decisions and bit-exact AMM pivoted-Cholesky
- * rank decisions (src/samplers/amm.jl:201-205) need identical exp/log/sincos on
+ * rank decisions (src/samplers/amm.jl:86-90) need identical exp/log/sincos on
  * host and device: ocml and glibc differ in the last ulp.  Everything here uses
  * only correctly rounded IEEE operations (+ - * / sqrt, explicit fma) and
  * integer arithmetic; build with -ffp-contract=off on both sides.

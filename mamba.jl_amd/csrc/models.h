@@ -377,7 +377,7 @@ struct Mdl<MMB_MODEL_LINE> {
   __device__ __forceinline__ static void gibbs(const SweepArgs& A, const DBlock& B, St& s, const Lc&,
                                const Grp<G>&, const mmb_rng* rn, const mmb_rng* gn,
                                const mmb_rng* gu, double) {
-    if (B.nodes[0] == MMB_LINE_BETA) {  // line.jl:168-177
+    if (B.nodes[0] == MMB_LINE_BETA) {  // line.jl:27-36
       double s2 = s.v[2];
       double sb = sqrt(1000.0);
       double ic = 1.0 / (sb * sb);
@@ -396,7 +396,7 @@ struct Mdl<MMB_MODEL_LINE> {
       mmb_normal_pair(rn, 0u, &z0, &z1);
       s.v[0] = m1 + l11 * z0;
       s.v[1] = m2 + (l21 * z0 + l22 * z1);
-    } else {  // line.jl:179-186
+    } else {  // line.jl:38-45
       double ssq = 0.0;
 #pragma unroll
       for (int i = 0; i < 5; ++i) {

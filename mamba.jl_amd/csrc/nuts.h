@@ -22,12 +22,14 @@
 // for the direction, 1 uniform per merge (only when the first half's s is true), 1 top-level
 // uniform only if T.s (the `&&` short-circuit of nuts.jl:117).  nutsepsilon (nuts.jl:192-205)
 // consumes d normals of the INIT substream at the first update.  Depth is capped at
-// MMB_NUTS_MAX_DEPTH (reference: unbounded), identically in oracle/oracle.c.
+// MMB_NUTS_MAX_DEPTH = 16 (65536 leapfrogs; reference: unbounded), identically in
+// oracle/oracle.c; every update that reaches the cap with the trajectory still growing is
+// counted (Env::stat[1], mmb_nuts_stats), so a run shows whether the cap ever acted.
 #pragma once
 #include "device.h"
 
 #ifndef MMB_NUTS_MAX_DEPTH
-#define MMB_NUTS_MAX_DEPTH 10
+#define MMB_NUTS_MAX_DEPTH 16
 #endif
 #define MMB_NUTS_NSLOT (MMB_NUTS_MAX_DEPTH + 1)
 
@@ -74,6 +76,7 @@ struct Nuts {
     double target;
     mmb_rng rn, ru, ri;
     double* F;         // this chain's frames
+    unsigned long long* stat;  // null or {updates, depth-cap hits, sum of tree depths}
   };
 
   // dot1 / nouturn of oracle.c: sequential (mul then add) within a lane, then the group sum
@@ -210,6 +213,10 @@ struct Nuts {
               p = mmb_exp(-0.75 * mmb_log(m));
               S.t_epsbar = mmb_exp(p * mmb_log(S.t_eps) + (1.0 - p) * mmb_log(S.t_epsbar));
             }
+            if (E.stat && E.lane == 0) {
+              atomicAdd(&E.stat[0], 1ull);
+              atomicAdd(&E.stat[2], (unsigned long long)S.j);
+            }
             S.pc = NPC_DONE;
             return false;
           }
@@ -308,7 +315,10 @@ struct Nuts {
           S.s = S.cs && nouturn(g, S.xm, S.xp, S.rm, S.rp, d);
           S.t_alpha = S.calpha;
           S.t_nalpha = S.cnalpha;
-          if (S.j >= MMB_NUTS_MAX_DEPTH) S.s = 0;
+          if (S.j >= MMB_NUTS_MAX_DEPTH && S.s) {  // the reference would keep doubling
+            if (E.stat && E.lane == 0) atomicAdd(&E.stat[1], 1ull);
+            S.s = 0;
+          }
           S.pc = NPC_DOUBLE;
           continue;
         }

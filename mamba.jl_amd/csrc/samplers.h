@@ -470,7 +470,7 @@ struct Smp {
   }
 
   // ---------------------------------------------------------------- AMM
-  // amm.jl:181-223.  LDS per chain: mat[TP] | z2[DP] | vv[DP] | mv[DP] | ia[2*DP ints]
+  // amm.jl:66-108.  LDS per chain: mat[TP] | z2[DP] | vv[DP] | mv[DP] | ia[2*DP ints]
   __device__ __forceinline__ static void amm(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,
                              const mmb_rng& ru, bool adapt, St& s, const Lc& l, const Grp<G>& g,
                              double* lds, double upre) {
@@ -588,7 +588,7 @@ struct Smp {
       for (int r = 0; r < R; ++r) v[r] = x[r];
     }
     MMB_PROF_MARK(3, g.lane)
-    if (adapt) {  // amm.jl:196-206
+    if (adapt) {  // amm.jl:81-91
       m += 1;
       const double p = (double)m / ((double)m + 1.0);
       const double q = 1.0 - p;
@@ -699,7 +699,7 @@ struct Smp {
   __device__ __forceinline__ static double width(const DBlock& B, int e) {
     return B.width ? B.width[e] : B.width0;
   }
-  // slice.jl:271-297 (Univariate)
+  // slice.jl:66-92 (Univariate)
   __device__ __forceinline__ static void slice_uni(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
                                    const Lc& l, const Grp<G>& g) {
     const int d = B.d;
@@ -741,7 +741,7 @@ struct Smp {
     }
     M::relist(B, s, g, x);
   }
-  // slice.jl:300-322 (Multivariate)
+  // slice.jl:95-117 (Multivariate)
   __device__ __forceinline__ static void slice_multi(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
                                      const Lc& l, const Grp<G>& g) {
     const int d = B.d;
@@ -801,6 +801,7 @@ struct Smp {
     E.ru = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_UNIFORM);
     E.ri = mmb_rng_make(A.seed, chain, (uint32_t)it, (uint32_t)b, MMB_SUB_INIT);
     E.F = B.t_nfr + (size_t)c * NutsFrames<NU::DV>::DBL;
+    E.stat = A.nuts_stat;
     while (NU::advance(S, E, g)) S.lf = M::logf_grad(A, B, s, S.x, S.g);
     double* tw = B.t_nuts + (size_t)c * 8;
     if (g.lane == 0) {
@@ -813,7 +814,7 @@ struct Smp {
   }
 
   // ---------------------------------------------------------------- HMC / MALA
-  // sample!(v::HMCVariate) (hmc.jl:72-111) / sample!(v::MALAVariate) (mala.jl:67-90), hmc.h
+  // sample!(v::HMCVariate) (hmc.jl:72-111) / sample!(v::MALAVariate) (mala.jl:67-86), hmc.h
   // machines with the model gradient computed inline; tune (epsilon, L) is per chain.
   template <bool MALA>
   __device__ __forceinline__ static void hmc(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,

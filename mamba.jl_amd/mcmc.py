@@ -129,6 +129,13 @@ class Engine:
         self._chk(self.lib.mmb_grad_evals(self.h, C.byref(n)))
         return n.value
 
+    def nuts_stats(self):
+        """NUTS tree statistics since init_chains (mmb_nuts_stats): completed updates,
+        updates stopped by the depth cap (reference: unbounded), mean final tree depth."""
+        v = (C.c_int64 * 3)()
+        self._chk(self.lib.mmb_nuts_stats(self.h, v))
+        return {"updates": v[0], "depth_cap_hits": v[1], "depth_sum": v[2]}
+
     def state_bytes(self):
         b = C.c_double()
         self.lib.mmb_state_bytes(self.h, C.byref(b))

@@ -150,7 +150,7 @@ def logistic(nobs, ncoef, prior_sd=10.0):
 
 
 # ---- reference data / inits ------------------------------------------------------
-LINE_DATA = {"x": [1.0, 2, 3, 4, 5], "y": [1.0, 3, 3, 3, 5]}           # line.jl:210-214
+LINE_DATA = {"x": [1.0, 2, 3, 4, 5], "y": [1.0, 3, 3, 3, 5]}           # line.jl:69-73
 
 RATS_Y = [151, 199, 246, 283, 320, 145, 199, 249, 293, 354, 147, 214, 263, 312, 328,
           155, 200, 237, 272, 297, 135, 188, 230, 280, 323, 159, 210, 252, 298, 331,
@@ -198,7 +198,7 @@ def rats_init_ls(chains, seed=1):
 
 
 def line_init_matrix(chains, seed=123):
-    """line.jl:222-229: beta ~ Normal(0,1) x2, s2 ~ Gamma(1,1) (numpy stream, not MT)."""
+    """line.jl:81-88: beta ~ Normal(0,1) x2, s2 ~ Gamma(1,1) (numpy stream, not MT)."""
     rng = np.random.default_rng(seed)
     out = np.empty((chains, 3))
     out[:, :2] = rng.normal(0.0, 1.0, (chains, 2))

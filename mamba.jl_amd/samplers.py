@@ -11,7 +11,7 @@ Argument meaning, defaults and validation errors follow the reference:
   HMC(params, epsilon, L[, Sigma]; dtype=:forward)            src/samplers/hmc.jl:47-65
   MALA(params, epsilon[, Sigma]; dtype=:forward)              src/samplers/mala.jl:43-58
   Gibbs(params)  -- a user `Sampler(params, f)` whose f is the node's conjugate full
-                    conditional (doc/tutorial/line.jl:168-186); lowered per model.
+                    conditional (doc/tutorial/line.jl:27-45); lowered per model.
 """
 import numpy as np
 
@@ -57,7 +57,7 @@ class Sampler:
         self.targets = []
 
     def validate(self, dim):
-        """validate(v) (amwg.jl:37-42, amm.jl:150-155, slice.jl:237-247)"""
+        """validate(v) (amwg.jl:37-42, amm.jl:35-40, slice.jl:37-42)"""
         t = self.tuning
         if self.kind == abi.MMB_SAMPLER_AMWG and not (t.size == 1 or t.size == dim):
             raise ArgumentError(f"length(sigma) differs from variate length {dim}")

@@ -42,7 +42,7 @@ LINE_SCHEMES = {
     "gibbs": lambda M: [M.Gibbs("beta"), M.Gibbs("s2")],
     "amwg_slice": lambda M: [M.AMWG("beta", 1.0), M.Slice("s2", 3.0, transform=True)],
     "nuts": lambda M: [M.NUTS(["beta", "s2"])],
-    "nuts_slice": lambda M: [M.NUTS("beta"), M.Slice("s2", 3.0)],        # doc/tutorial/line.jl:53-56
+    "nuts_slice": lambda M: [M.NUTS("beta"), M.Slice("s2", 3.0)],        # doc/tutorial/line.jl:49-50
     "hmc": lambda M: [M.HMC(["beta", "s2"], 0.05, 8)],
     "hmc_sigma_slice": lambda M: [M.HMC("beta", 0.1, 5, np.array([[1.6, -0.45], [-0.45, 0.15]])),
                                   M.Slice("s2", 3.0)],
@@ -158,7 +158,7 @@ LOGISTIC_GRAD_SCHEMES = {
 
 @pytest.mark.parametrize("name", sorted(LOGISTIC_GRAD_SCHEMES))
 def test_logistic_hmc_mala_parity(mamba, oracle, name):
-    """HMC / MALA (hmc.jl:72-111, mala.jl:67-90) on the batched MFMA gradient engine:
+    """HMC / MALA (hmc.jl:72-111, mala.jl:67-86) on the batched MFMA gradient engine:
     bit-exact against the oracle (same gradient summation spec as NUTS)."""
     m, _ = logistic(mamba, 1000, 50, LOGISTIC_GRAD_SCHEMES[name](mamba, 50))
     K = 100

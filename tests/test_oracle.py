@@ -144,7 +144,7 @@ def test_line_posterior_statistical(mamba, oracle, scheme):
          "gibbs": [mamba.Gibbs("beta"), mamba.Gibbs("s2")],
          "slice": [mamba.Slice(["beta", "s2"], [3.0, 1.0, 2.0], mamba.Univariate)],
          "nuts": [mamba.NUTS(["beta", "s2"])],
-         "nuts_slice": [mamba.NUTS("beta"), mamba.Slice("s2", 3.0)]}[scheme]   # doc/tutorial/line.jl:53-56
+         "nuts_slice": [mamba.NUTS("beta"), mamba.Slice("s2", 3.0)]}[scheme]   # doc/tutorial/line.jl:49-50
     m = line_model(mamba, S)
     init = mamba.model.line_init_matrix(64)
     st = oracle.new_state(m, init)
@@ -192,7 +192,7 @@ S_HMC = np.array([[1.0, 0.2], [0.2, 0.5]])
 
 @pytest.mark.parametrize("scheme", ["hmc", "hmc_sigma", "mala", "mala_sigma"])
 def test_line_hmc_mala_gaussian_conditional(mamba, oracle, scheme):
-    """HMC (hmc.jl:72-111) and MALA (mala.jl:67-90), with SigmaL = I and with a Sigma, on
+    """HMC (hmc.jl:72-111) and MALA (mala.jl:67-86), with SigmaL = I and with a Sigma, on
     the exact Gaussian beta | s2 (as test_line_nuts_gaussian_conditional)."""
     S = {"hmc": mamba.HMC("beta", 0.1, 16), "hmc_sigma": mamba.HMC("beta", 0.1, 16, S_HMC),
          "mala": mamba.MALA("beta", 0.02), "mala_sigma": mamba.MALA("beta", 0.6, C_LINE)}[scheme]
