@@ -41,6 +41,10 @@ extern "C" {
 #define MMB_E_HIP (-3)         /* HIP runtime error */
 #define MMB_E_STATE (-4)       /* call out of order (e.g. run before init) */
 #define MMB_E_NOMEM (-5)
+/* Slice shrinkage bound: the reference shrinks until it accepts (slice.jl:78-88,103-113); a
+ * kernel must end, so an update still rejecting after this many candidates stops and mmb_run
+ * returns MMB_E_STATE (only a degenerate target, e.g. an infinite width, gets there). */
+#define MMB_SLICE_MAX_SHRINK 100000
 
 /* ---- lowered model kinds ---- */
 typedef enum {

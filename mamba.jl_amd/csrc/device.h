@@ -81,7 +81,8 @@ struct SweepArgs {
   int64_t kept_base;     // kept rows before this launch (within the mmb_run window)
   int64_t kept_origin;   // kept count at the window start (rows are relative to the window)
   double* vals;          // model-specific device layout
-  unsigned long long* nuts_stat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat)
+  unsigned long long* nuts_stat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat),
+                                  // [3] Slice updates stopped at MMB_SLICE_MAX_SHRINK
   double* draws;         // [n_kept][pmon][K] or null
   const double* data0;   // model data (rats: y[150]; line: x[5], y[5] packed as 10)
   double ig_c;           // 0.001 log(0.001) - lgamma(0.001)

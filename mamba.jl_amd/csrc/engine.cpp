@@ -76,7 +76,9 @@ struct mmb_engine {
   int64_t* lg_itc = nullptr;
   int64_t lg_steps = 0;  // gradient steps of the last window
   unsigned long long* lg_ngrad = nullptr;
-  unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum} since init_chains
+  unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum}, Slice overflows
+                                          // since init_chains
+  unsigned long long slice_overflows = 0;  // d_nstat[3] as last reported by mmb_run
   // draws of the last window
   double* d_draws = nullptr;
   size_t draws_cap = 0;
@@ -432,6 +434,8 @@ int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device
   if (ir->nnodes < 1 || !ir->nodes || ir->ncode < 1 || !ir->code || ir->npool < 0 || (ir->npool > 0 && !ir->pool) ||
       ir->nconst < 0 || (ir->nconst > 0 && !ir->consts) || ir->nmon < 0 || (ir->nmon > 0 && !ir->mon))
     return fail(nullptr, MMB_E_ARG, "node IR: missing tables");
+  if (ir->npool >= (1 << 24) || ir->nconst >= (1 << 24))  // code-word operands are 24-bit
+    return fail(nullptr, MMB_E_UNSUPPORTED, "node IR: pool and constant tables must hold < 2^24 entries");
   if (ir->stack < 1 || ir->stack > MMB_IR_MAX_STACK)
     return fail(nullptr, MMB_E_ARG, "node IR: stack depth must be 1..%d", MMB_IR_MAX_STACK);
   int depth = 0;
@@ -717,8 +721,9 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
   e->iter = 0;
   e->n_kept = 0;
   HIPCHK(e, dalloc(&e->d_vals, (size_t)K * e->VS));
-  HIPCHK(e, dalloc(&e->d_nstat, 3));
-  HIPCHK(e, hipMemset(e->d_nstat, 0, 3 * sizeof(unsigned long long)));
+  e->slice_overflows = 0;
+  HIPCHK(e, dalloc(&e->d_nstat, 4));
+  HIPCHK(e, hipMemset(e->d_nstat, 0, 4 * sizeof(unsigned long long)));
   const size_t DP = e->DP, TP = e->TP;
   for (auto& h : e->blocks) {
     HIPCHK(e, dalloc(&h.m, K));
@@ -1007,6 +1012,18 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
   }
   e->iter = it0 + a->iters;
   e->n_kept = want ? nk : 0;
+  if ((e->kinds & (1u << MMB_SAMPLER_SLICE)) && a->iters > 0) {
+    unsigned long long ov = 0;
+    HIPCHK(e, hipMemcpyAsync(&ov, e->d_nstat + 3, sizeof ov, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (ov != e->slice_overflows) {
+      const unsigned long long n = ov - e->slice_overflows;
+      e->slice_overflows = ov;
+      return fail(e, MMB_E_STATE, "Slice: %llu update(s) in iterations %lld..%lld still rejected after %d shrink "
+                  "steps (the reference would loop forever; check the widths and the target's support)",
+                  n, (long long)it0 + 1, (long long)e->iter, MMB_SLICE_MAX_SHRINK);
+    }
+  }
   if (a->draws && nk > 0) {
     std::vector<double> h((size_t)nk * e->pmon * e->K);
     HIPCHK(e, hipMemcpyAsync(h.data(), e->d_draws, h.size() * sizeof(double), hipMemcpyDeviceToHost,

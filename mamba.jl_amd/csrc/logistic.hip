@@ -221,6 +221,9 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
 #define LG_RB 32   // rows per staged pass (two 16-row MFMA blocks)
 #define LG_LD 66   // padded LDS row stride (doubles)
 #define LG_PER (LG_RB * 64 / 256)  // doubles of a pass staged per thread
+// KS: MFMA k-steps of eta = X*B, ceil(p/4) rounded to 13 (p <= 52) or 16 (p <= MMB_LG_DV); the padded
+// coefficients are zero in X and in the positions, so both give the same sequential fma chain.
+template <int KS>
 __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs A, int parity) {
   __shared__ __attribute__((aligned(16))) double xs[LG_RB][LG_LD];
   __shared__ double ys[LG_RB];
@@ -238,9 +241,9 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
   const int lc = l & 15, lq = l >> 4;
   const int slot = ct * 64 + w * 16 + lc;
   const bool live = slot < nact;
-  double bpos[13];
+  double bpos[KS];
 #pragma unroll
-  for (int kk = 0; kk < 13; ++kk) bpos[kk] = live ? A.pos[(size_t)slot * 64 + 4 * kk + lq] : 0.0;
+  for (int kk = 0; kk < KS; ++kk) bpos[kk] = live ? A.pos[(size_t)slot * 64 + 4 * kk + lq] : 0.0;
   mmb_d4 tot[4], acc[4];
   double ltot = 0.0;
   const int rps = A.rps;
@@ -283,13 +286,13 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
       mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
       if (two) {
 #pragma unroll
-        for (int kk = 0; kk < 13; ++kk) {
+        for (int kk = 0; kk < KS; ++kk) {
           eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
           eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 + lc][4 * kk + lq], bpos[kk], eta1, 0, 0, 0);
         }
       } else {
 #pragma unroll
-        for (int kk = 0; kk < 13; ++kk)
+        for (int kk = 0; kk < KS; ++kk)
           eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
       }
       // residual terms of both blocks first (branch-free: padded rows have X = 0, eta = 0,
@@ -355,6 +358,10 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t
   return hipGetLastError();
 }
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {
-  hipLaunchKernelGGL(lg_grad_kernel, dim3(MMB_LG_NG * ((A.K + 63) / 64)), dim3(256), 0, st, A, parity);
+  const dim3 grid(MMB_LG_NG * ((A.K + 63) / 64)), blk(256);
+  if (A.p <= 52)
+    hipLaunchKernelGGL(lg_grad_kernel<13>, grid, blk, 0, st, A, parity);
+  else
+    hipLaunchKernelGGL(lg_grad_kernel<16>, grid, blk, 0, st, A, parity);
   return hipGetLastError();
 }

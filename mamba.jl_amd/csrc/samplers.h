@@ -696,6 +696,13 @@ struct Smp {
   }
 
   // ---------------------------------------------------------------- Slice
+  // The reference shrinks until it accepts (slice.jl:78-88,103-113); a kernel must end, so
+  // after MMB_SLICE_MAX_SHRINK rejections the update stops, the chain-update is counted in
+  // stat[3] and mmb_run fails with MMB_E_STATE (never a silent out-of-slice draw).  Only a
+  // degenerate target gets there (e.g. an infinite width: every candidate is NaN, -Inf).
+  __device__ __forceinline__ static void slice_overflow(const SweepArgs& A, const Grp<G>& g) {
+    if (g.lane == 0) atomicAdd(&A.nuts_stat[3], 1ull);
+  }
   __device__ __forceinline__ static double width(const DBlock& B, int e) {
     return B.width ? B.width[e] : B.width0;
   }
@@ -726,9 +733,10 @@ struct Smp {
         double xo = x[r];
         double u = mmb_uniform(&ru, k++);
         if (own) x[r] = lo[r] + (up[r] - lo[r]) * u;
-        for (int guard = 0; guard < 100000; ++guard) {
+        bool hit = false;
+        for (int guard = 0; guard < MMB_SLICE_MAX_SHRINK; ++guard) {
           logf0 = M::logf(A, B, s, l, g, x);
-          if (!(logf0 < p0)) break;
+          if (!(logf0 < p0)) { hit = true; break; }
           if (own) {
             double value = x[r];
             if (value < xo) lo[r] = value;
@@ -737,6 +745,7 @@ struct Smp {
           u = mmb_uniform(&ru, k++);
           if (own) x[r] = lo[r] + (up[r] - lo[r]) * u;
         }
+        if (!hit) slice_overflow(A, g);
       }
     }
     M::relist(B, s, g, x);
@@ -760,8 +769,9 @@ struct Smp {
       } else { lo[r] = up[r] = x[r] = 0.0; }
     }
     k = 1u + 2u * (uint32_t)d;
-    for (int guard = 0; guard < 100000; ++guard) {
-      if (!(M::logf(A, B, s, l, g, x) < p0)) break;
+    bool hit = false;
+    for (int guard = 0; guard < MMB_SLICE_MAX_SHRINK; ++guard) {
+      if (!(M::logf(A, B, s, l, g, x) < p0)) { hit = true; break; }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         int e = r * G + g.lane;
@@ -774,6 +784,7 @@ struct Smp {
       }
       k += (uint32_t)d;
     }
+    if (!hit) slice_overflow(A, g);
     M::relist(B, s, g, x);
   }
 

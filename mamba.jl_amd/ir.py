@@ -301,6 +301,14 @@ class _Lowering:
         self.consts.append(float(v))
         return len(self.consts) - 1
 
+    @staticmethod
+    def word(opc, arg):
+        """One code word: opcode in the top byte, operand (pool / value / constant offset) in
+        the low 24 bits; a larger operand would carry into the opcode, so it is refused."""
+        if not 0 <= arg < 1 << 24:
+            raise ArgumentError(f"node IR operand {arg} does not fit in 24 bits (pool or model too large)")
+        return opc << 24 | arg
+
     def put(self, key, arr):
         if key in self.pool_of:
             return self.pool_of[key]
@@ -380,7 +388,7 @@ class _Lowering:
             return sp + 1
 
         if isinstance(e, Const):
-            return push(op["const"] << 24 | self.const(e.v))
+            return push(self.word(op["const"], self.const(e.v)))
         if isinstance(e, Elem):
             k = self.kind(e.name)
             ln = self.length(Ref(e.name))
@@ -388,10 +396,10 @@ class _Lowering:
                 raise ArgumentError(f"{e.name}[{e.k}] out of range")
             if k == "param":
                 refs.add(e.name)
-                return push(op["val"] << 24 | (m.nodes[e.name].offset + e.k - 1))
+                return push(self.word(op["val"], (m.nodes[e.name].offset + e.k - 1)))
             if k in ("fixed", "data"):
                 v = m.fixed_vals[e.name] if k == "fixed" else m.inputs[e.name]
-                return push(op["datas"] << 24 | self.put(("elem", e.name, e.k), v[e.k - 1:e.k]))
+                return push(self.word(op["datas"], self.put(("elem", e.name, e.k), v[e.k - 1:e.k])))
             raise ArgumentError("element of a logical: index its parents instead")
         if isinstance(e, Ref):
             k = self.kind(e.name)
@@ -406,10 +414,10 @@ class _Lowering:
             if k == "param":
                 refs.add(e.name)
                 o = m.nodes[e.name].offset
-                return push((op["val"] if ln == 1 else op["vali"]) << 24 | o)
+                return push(self.word(op["val"] if ln == 1 else op["vali"], o))
             v = m.fixed_vals[e.name] if k == "fixed" else m.inputs[e.name]
             o = self.put(("v", e.name), v)
-            return push((op["datas"] if ln == 1 else op["data"]) << 24 | o)
+            return push(self.word(op["datas"] if ln == 1 else op["data"], o))
         if isinstance(e, Gather):
             if e.idx not in m.inputs:
                 raise ArgumentError(f"gather index {e.idx} must be an input (data) vector")
@@ -423,12 +431,12 @@ class _Lowering:
             if k == "param":
                 refs.add(e.name)
                 w = self.put(("idx", e.idx), idx - 1.0)
-                sp2 = push(op["valg"] << 24 | m.nodes[e.name].offset)
+                sp2 = push(self.word(op["valg"], m.nodes[e.name].offset))
                 self.code.append(w)
                 return sp2
             if k in ("fixed", "data"):
                 v = m.fixed_vals[e.name] if k == "fixed" else m.inputs[e.name]
-                return push(op["data"] << 24 | self.put(("g", e.name, e.idx), v[(idx - 1).astype(int)]))
+                return push(self.word(op["data"], self.put(("g", e.name, e.idx), v[(idx - 1).astype(int)])))
             raise ArgumentError("gather from a logical: gather its parents instead")
         if isinstance(e, Bin):
             sp = self.emit(e.a, n, sp, refs)

@@ -363,3 +363,66 @@ def test_logistic_single_chain(mamba, oracle):
     eng, dg, st, do = both(mamba, oracle, m, init, 12, 4, 2, model_burnin=6)
     np.testing.assert_array_equal(dg, do)
     np.testing.assert_array_equal(eng.values(), st["values"])
+
+
+def test_logistic_nuts_parity_full(mamba, oracle):
+    """Config 4 at its stated size (N = 10000, p = 50; BASELINE configs[3], nuts.jl:95-180):
+    mmb_lg_rps = 160 rows per sub-range, 32 groups x 2 sub-ranges; 70 chains = one full and
+    one partly filled 64-chain tile, NUTS chains idle at different steps.  Bit-exact."""
+    m, _ = logistic(mamba, 10000, 50)
+    K = 70
+    init = np.random.default_rng(21).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 8, 2, 1, model_burnin=4)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+
+
+@pytest.mark.parametrize("p", [53, 64])
+def test_logistic_wide_parity(mamba, oracle, p):
+    """53 <= p <= MMB_LG_DV: the 16-k-step first GEMM (coefficients 52..63 are part of eta)."""
+    for sch in ([mamba.NUTS("beta")], [mamba.HMC("beta", 0.01, 5)]):
+        m, _ = logistic(mamba, 1000, p, sch)
+        K = 40
+        init = np.random.default_rng(p).normal(0.0, 0.1, (K, p))
+        eng, dg, st, do = both(mamba, oracle, m, init, 10, 2, 1, model_burnin=5)
+        np.testing.assert_array_equal(dg, do)
+        np.testing.assert_array_equal(eng.values(), st["values"])
+        assert np.abs(dg[-1] - dg[0]).max() > 0
+
+
+def test_logistic_full_size_properties(mamba):
+    """Config 4 at full size: N = 10000, p = 50, 4096 chains.  Finite draws, every update
+    completed without hitting the depth cap, gradient count consistent with the tree
+    depths, and Gelman-Rubin PSRF < 1.1 on all 50 coefficients after burnin."""
+    m, _ = logistic(mamba, 10000, 50)
+    K = 4096
+    eng = mamba.Engine(m)
+    eng.init_chains(np.random.default_rng(5).normal(0.0, 0.1, (K, 50)), seed=6)
+    d = eng.run(200, burnin=100, thin=1, model_burnin=100, keep_device=True)
+    assert d.shape == (100, 50, K) and np.isfinite(d).all()
+    ns = eng.nuts_stats()
+    assert ns["updates"] == 200 * K and ns["depth_cap_hits"] == 0
+    # a depth-j tree evaluates at least j leapfrog gradients (one per doubling)
+    assert eng.grad_evals() >= ns["depth_sum"] and 1.0 <= ns["depth_sum"] / ns["updates"] <= 10.0
+    psrf, _ = mamba.gelmandiag_sharded(eng)
+    assert (psrf[:, 0] < 1.1).all(), psrf[:, 0].max()
+
+
+@pytest.mark.parametrize("form", ["uni", "multi"])
+def test_slice_shrink_overflow_is_an_error(mamba, form):
+    """An infinite Slice width makes every candidate NaN (lower = -Inf, upper = NaN), which
+    s2's InverseGamma support rejects: the reference's shrink loop (slice.jl:78-88,103-113)
+    never ends.  The kernel stops after MMB_SLICE_MAX_SHRINK rejections and mmb_run reports
+    MMB_E_STATE instead of keeping an out-of-slice draw silently."""
+    Fm = mamba.Univariate if form == "uni" else mamba.Multivariate
+    m = line(mamba, [mamba.AMWG("beta", 1.0), mamba.Slice("s2", np.inf, Fm)])
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.line_init_matrix(3, seed=1), seed=2)
+    with pytest.raises(RuntimeError, match=r"error -4 .*Slice: 3 update\(s\) in iterations 1\.\.1"):
+        eng.run(1, burnin=0, thin=1)
+    # a finite width on the same engine and chains still runs
+    m2 = line(mamba, [mamba.AMWG("beta", 1.0), mamba.Slice("s2", 3.0, Fm)])
+    e2 = mamba.Engine(m2)
+    e2.init_chains(mamba.model.line_init_matrix(3, seed=1), seed=2)
+    assert np.isfinite(e2.run(5, burnin=0, thin=1)).all()

@@ -217,6 +217,12 @@ def test_ir_lowering_errors(mamba):
     mm.setinputs({"x": [1.0, 2, 3]}).setsamplers([mamba.AMWG("mu", 1.0)])
     with pytest.raises(mamba.ArgumentError, match="length"):
         mm.init_matrix([{"y": [1.0, 2, 3], "mu": [0.0, 1.0]}], 1)
+    # code-word operands are 24 bits: a pool offset >= 2^24 would carry into the opcode
+    W = mamba.ir._Lowering.word
+    assert W(5, (1 << 24) - 1) == (5 << 24) | 0xffffff
+    for bad_arg in (1 << 24, -1):
+        with pytest.raises(mamba.ArgumentError, match="24 bits"):
+            W(5, bad_arg)
 
 
 def test_ir_create_validates_before_touching_the_device(mamba):
