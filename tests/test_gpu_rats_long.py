@@ -1,0 +1,72 @@
+"""Config 3 at the rats.rst run length on the GPU (doc/examples/rats.rst:37-52: 10000
+iterations, burnin 2500, thin 2), 16384 chains per scheme, against the published summaries
+(tests/golden/rats_published.json).  Chain means come from the on-device per-chain sums
+(mmb_chain_summary), so the 2 GB of kept draws never leave HBM; our standard error is the
+between-chain SD of those means / sqrt(K).
+
+* reference scheme Slice + AMWG (rats.jl:112-116) and the Gibbs + AMM scheme with the AMM
+  blocks frozen (adapt=:none): s2_c, mu_beta, alpha0 within 5 combined MCSE of the
+  published means;
+* Gibbs + AMM with adapt=:all (the headline workload): mu_beta and alpha0 within 5 MCSE;
+  s2_c is biased LOW.  That is a property of the always-adapting proposal of
+  amm.jl:73-91, not of this engine: tools/amm_numpy_check.py, an independent numpy
+  restatement (LAPACK-free plain Cholesky of the same Sigma, numpy RNG), shows the same
+  drop, also when adaptation starts from a converged chain, and the slow recovery as the
+  adapted covariance grows.  The test pins the size of the effect so that a
+  change in it is noticed."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PUB = json.load(open(os.path.join(HERE, "golden", "rats_published.json")))
+NAMES = ["s2_c", "mu_beta", "alpha0"]
+
+
+def run(mamba, scheme, K=16384, iters=10000, burnin=2500, thin=2, seed=20261016):
+    m = mamba.rats()
+    m.setinputs(mamba.model.RATS_DATA)
+    m.setsamplers(scheme)
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(K, seed=1), seed=seed)
+    eng.run(iters, burnin=burnin, thin=thin, keep_device=True)
+    n = eng.num_kept()
+    assert n == (iters - burnin) // thin
+    shift = np.array([PUB["mean"][k] for k in NAMES])
+    s1 = eng.chain_summary(shift, 100, 0)[:, :, 0]          # F_S1: per-chain shifted sums
+    cm = shift + s1 / n                                       # K x 3 chain means
+    eng.close()
+    assert np.isfinite(cm).all()
+    return cm.mean(0), cm.std(0) / np.sqrt(K)
+
+
+def _within(mean, se, names, nsig=5.0):
+    for j, k in enumerate(NAMES):
+        if k not in names:
+            continue
+        tol = nsig * np.hypot(PUB["mcse"][k], se[j])
+        assert abs(mean[j] - PUB["mean"][k]) < tol, (k, mean[j], PUB["mean"][k], tol)
+
+
+@pytest.mark.parametrize("scheme", ["reference", "gibbs_amm_frozen"])
+def test_rats_published_summaries(mamba, scheme):
+    if scheme == "reference":
+        sch = mamba.model.rats_scheme_reference()
+    else:
+        G = mamba.Gibbs
+        sch = [G("s2_c"), mamba.AMM("alpha", np.eye(30), adapt="none"), G("mu_alpha"), G("s2_alpha"),
+               mamba.AMM("beta", 0.01 * np.eye(30), adapt="none"), G("mu_beta"), G("s2_beta")]
+    mean, se = run(mamba, sch)
+    _within(mean, se, NAMES)
+
+
+def test_rats_gibbs_amm_adaptive(mamba):
+    mean, se = run(mamba, mamba.model.rats_scheme_gibbs_amm())
+    _within(mean, se, ["mu_beta", "alpha0"])
+    # the adaptive-AMM s2_c deficit (published 37.25, MCSE 0.23): measured 34.5 at this
+    # length with 16384 chains (SE 0.02); the numpy restatement gives 32-34 at 8000-12000
+    assert 32.5 < mean[0] < 36.0, mean[0]
