@@ -290,24 +290,32 @@ def main():
         after = eng.nuts_stats()
         nuts_timed = {k: after[k] - nuts_before[k] for k in after}
 
-    psrf = None
-    # Gelman-Rubin over all chains of all GPUs: device partials + one RCCL all-reduce
-    def ar_sum(x):
-        if world == 1:
-            return x
-        t = torch.tensor(x, dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t)
-        return t.cpu().numpy()
+    # Gelman-Rubin over all chains of all GPUs: device partials + the library's own RCCL
+    # communicator (mmb_comm_init / mmb_range_allreduce / mmb_gr_allreduce, the C-ABI collective
+    # a Julia caller uses); rank 0's unique id travels over the launcher's process group.
+    # MMB_DIST_BACKEND=gloo (several ranks sharing one GPU, which RCCL refuses) reduces the same
+    # device partials through torch.distributed on the host instead.
+    if backend == "nccl":
+        uid = [mb.Comm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = mb.Comm([eng], nranks=world, rank0=rank, uid=uid[0])
+        psrf, _ = mb.gelmandiag_rccl(comm)
+        comm.close()
+    else:
+        def ar_sum(x):
+            t = torch.tensor(x, dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t)
+            return t.cpu().numpy()
 
-    def ar_minmax(lo, hi):
-        if world == 1:
-            return lo, hi
-        a = torch.tensor(np.concatenate([-lo, hi]), dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(a, op=dist.ReduceOp.MAX)
-        a = a.cpu().numpy()
-        return -a[:len(lo)], a[len(lo):]
+        def ar_minmax(lo, hi):
+            a = torch.tensor(np.concatenate([-lo, hi]), dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(a, op=dist.ReduceOp.MAX)
+            a = a.cpu().numpy()
+            return -a[:len(lo)], a[len(lo):]
 
-    psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax)
+        psrf, _ = mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum if world > 1 else None,
+                                        allreduce_minmax=ar_minmax if world > 1 else None)
 
     # roofline of the dominant kernel; per-launch device time from HIP events on the engine's
     # stream, over full launches in the same steady state as the timed window
@@ -362,7 +370,7 @@ def main():
                  else
                  "synthetic X ~ N(0,1), y ~ Bernoulli(invlogit(X beta_true)) (SURVEY §8d seeds); inits N(0, 0.1^2)"),
         "config": {"workload": desc, "chains_per_gpu": K, "global_chains": K * world, "thin": thin,
-                   "parallelism": f"chain-shard x{world}", "collective": "rccl" if backend == "nccl" else backend},
+                   "parallelism": f"chain-shard x{world}", "collective": ("rccl (mmb_gr_allreduce)" if backend == "nccl" else backend)},
         "roofline": roof,
     }
     if args.workload != "rats":

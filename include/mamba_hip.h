@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 3
+#define MMB_ABI_VERSION 4
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -41,6 +41,7 @@ extern "C" {
 #define MMB_E_HIP (-3)         /* HIP runtime error */
 #define MMB_E_STATE (-4)       /* call out of order (e.g. run before init) */
 #define MMB_E_NOMEM (-5)
+#define MMB_E_COMM (-6)        /* RCCL error in a cross-GPU collective (mmb_comm_*, mmb_gr_allreduce) */
 /* Slice shrinkage bound: the reference shrinks until it accepts (slice.jl:78-88,103-113); a
  * kernel must end, so an update still rejecting after this many candidates stops and mmb_run
  * returns MMB_E_STATE (only a degenerate target, e.g. an infinite width, gets there). */
@@ -247,6 +248,31 @@ int mmb_get_draws(mmb_engine* e, double* draws);
 int mmb_gr_range(mmb_engine* e, double* minmax /* 2*p */);
 int64_t mmb_gr_len(const mmb_engine* e);
 int mmb_gr_partials(mmb_engine* e, const int32_t* link_kind, const double* shift, double* out);
+
+/* The one cross-GPU exchange (gelmandiag.jl:11-25), over RCCL/xGMI, inside the
+ * library so a ccall caller reaches it (SURVEY §8b mmb_gr_allreduce).  Chains never interact
+ * while sampling (mcmc.jl:48-52), so this is the only collective.
+ * A communicator spans the engines (one per GPU) of every participating process:
+ *   one process driving all GPUs (Julia threads / async streams):
+ *       mmb_comm_init(engines, ngpu, ngpu, 0, NULL, &c)          -> ncclCommInitAll
+ *   one process per GPU (torchrun-style, or Julia workers):
+ *       rank 0: mmb_comm_id(id); the caller broadcasts the MMB_COMM_ID_BYTES bytes;
+ *       every process: mmb_comm_init(&e, 1, nranks, rank, id, &c) -> ncclCommInitRank
+ *   (nlocal engines of one process take ranks rank0 .. rank0+nlocal-1 of nranks).
+ * mmb_range_allreduce: global [min, max] per monitored param (one MAX all-reduce of
+ *   (-min, max)), for link() (chains.jl:237-246) and the shift.
+ * mmb_gr_allreduce: mmb_gr_partials of every local engine (same link/shift on every rank),
+ *   summed over all ranks by one SUM all-reduce of mmb_gr_len doubles; out = global sums,
+ *   from which the host evaluates the PSRF as gelmandiag.jl:26-60 (mamba.jl_amd/gelman.py
+ *   psrf_from_sums).  Every rank must call each collective (RCCL semantics).
+ * Errors are reported through mmb_last_error(engines[0]). */
+#define MMB_COMM_ID_BYTES 128
+typedef struct mmb_comm mmb_comm;
+int mmb_comm_id(uint8_t* id /* MMB_COMM_ID_BYTES */);
+int mmb_comm_init(mmb_engine** engines, int nlocal, int nranks, int rank0, const uint8_t* id, mmb_comm** out);
+int mmb_range_allreduce(mmb_comm* c, double* minmax /* 2*p: [min, max] per param */);
+int mmb_gr_allreduce(mmb_comm* c, const int32_t* link_kind, const double* shift, double* out);
+void mmb_comm_destroy(mmb_comm* c);
 
 /* Posterior summaries of the device-kept draws, pooled over chains.
  * mmb_chain_summary replaces the per-element work of summarystats(c; etype=:bm)

@@ -1,0 +1,385 @@
+# MambaHIP.jl — the Julia side of the drop-in boundary (SURVEY §8b): ccall bindings of
+# include/mamba_hip.h plus the lowering of a Mamba `Model` to an mmb_model_spec, the packing
+# of the samplers' tune objects to the engine's canonical tune rows and back, and the branch
+# that `mcmc_master!` (src/model/mcmc.jl:36-59) gains.
+#
+# Julia 0.5 syntax, like the reference.  No Julia toolchain exists in the build image, so this
+# file is not executed here: it is the code a maintainer adds as src/hip/MambaHIP.jl and
+# `include`s from src/Mamba.jl.  Its tested mirror is the Python host package:
+#   lower        <-> mamba.jl_amd/model.py  Model.spec() / samplers.py
+#   pack_tune    <-> the canonical tune layout of engine.cpp mmb_get_tune / mmb_set_tune
+#   run_chains!  <-> mamba.jl_amd/mcmc.py  mcmc() / mcmc_restart()
+#   gelmandiag   <-> mamba.jl_amd/gelman.py gelmandiag_rccl() (mmb_comm_* / mmb_gr_allreduce)
+module MambaHIP
+
+using Mamba
+import Mamba: Model, Sampler, ModelState, ModelChains, Chains, AMWGTune, AMMTune, NUTSTune,
+              SliceTune, HMCTune, MALATune, SamplerTune, relist!, unlist, gettune
+
+const libmambahip = "libmambahip"              # on LD_LIBRARY_PATH / DL_LOAD_PATH
+
+# ---- constants of include/mamba_hip.h -----------------------------------------------------
+const MMB_E_UNSUPPORTED = Int32(-2)
+const MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = Int32(1), Int32(2), Int32(3)
+const MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE = Int32(1), Int32(2), Int32(3), Int32(4)
+const MMB_SAMPLER_GIBBS, MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = Int32(5), Int32(6), Int32(7)
+const MMB_ADAPT = Dict(:all => Int32(0), :burnin => Int32(1), :none => Int32(2))
+const MMB_COMM_ID_BYTES = 128
+
+# ---- structs (layout-checked against the header by tests/test_abi.py on the Python side) ----
+immutable BlockSpec                      # mmb_block_spec
+  sampler::Int32; nnodes::Int32; nodes::NTuple{4,Int32}
+  adapt::Int32; form::Int32; transform::Int32; batchsize::Int32
+  target::Float64; beta::Float64; scale::Float64
+  dim::Int32; ntuning::Int32; tuning::Ptr{Float64}
+  epsilon::Float64; nsteps::Int32; reserved::Int32
+end
+const NOBLOCK = BlockSpec(0, 0, (0, 0, 0, 0), 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 0, C_NULL, 0.0, 0, 0)
+
+immutable ModelSpec                      # mmb_model_spec
+  model::Int32; nblocks::Int32; blocks::NTuple{8,BlockSpec}
+  nobs::Int32; ncoef::Int32; prior_sd::Float64; reserved::NTuple{8,Int32}
+end
+
+type RunArgs                             # mmb_run_args (passed by reference)
+  iters::Int64; burnin::Int64; thin::Int64; model_burnin::Int64
+  draws::Ptr{Float64}; keep_device::Int32; time_kernels::Int32
+end
+
+# ---- raw bindings --------------------------------------------------------------------------
+last_error(e) = unsafe_string(ccall((:mmb_last_error, libmambahip), Cstring, (Ptr{Void},), e))
+check(rc, e) = rc == 0 ? nothing :
+  throw(rc == -1 ? ArgumentError(last_error(e)) : ErrorException("libmambahip error $rc: " * last_error(e)))
+
+function create(spec::ModelSpec, device::Integer)
+  h = Ref{Ptr{Void}}(C_NULL)
+  rc = ccall((:mmb_create, libmambahip), Cint, (Ref{ModelSpec}, Cint, Ref{Ptr{Void}}), spec, device, h)
+  rc == MMB_E_UNSUPPORTED && return nothing          # not lowered: the caller keeps the Julia path
+  check(rc, C_NULL); h[]
+end
+destroy(e) = ccall((:mmb_destroy, libmambahip), Void, (Ptr{Void},), e)
+set_data!(e, name::AbstractString, x::Vector{Float64}) =
+  check(ccall((:mmb_set_data, libmambahip), Cint, (Ptr{Void}, Cstring, Ptr{Float64}, Int64),
+              e, name, x, length(x)), e)
+num_values(e)    = ccall((:mmb_num_values, libmambahip), Cint, (Ptr{Void},), e)
+num_monitored(e) = ccall((:mmb_num_monitored, libmambahip), Cint, (Ptr{Void},), e)
+init_chains!(e, init::Matrix{Float64}, offset::Integer, seed::UInt64) =   # P x K (column = chain)
+  check(ccall((:mmb_init_chains, libmambahip), Cint, (Ptr{Void}, Ptr{Float64}, Int64, Int64, UInt64),
+              e, init, size(init, 2), offset, seed), e)
+run!(e, a::RunArgs) = check(ccall((:mmb_run, libmambahip), Cint, (Ptr{Void}, Ref{RunArgs}), e, a), e)
+get_values!(e, v::Matrix{Float64}) =
+  check(ccall((:mmb_get_values, libmambahip), Cint, (Ptr{Void}, Ptr{Float64}), e, v), e)
+tune_len(e) = ccall((:mmb_tune_len, libmambahip), Int64, (Ptr{Void},), e)
+get_tune!(e, t::Matrix{Float64}) = check(ccall((:mmb_get_tune, libmambahip), Cint, (Ptr{Void}, Ptr{Float64}), e, t), e)
+set_tune!(e, t::Matrix{Float64}) = check(ccall((:mmb_set_tune, libmambahip), Cint, (Ptr{Void}, Ptr{Float64}), e, t), e)
+set_iter!(e, it::Integer) = check(ccall((:mmb_set_iter, libmambahip), Cint, (Ptr{Void}, Int64), e, it), e)
+gr_len(e) = ccall((:mmb_gr_len, libmambahip), Int64, (Ptr{Void},), e)
+num_kept(e) = ccall((:mmb_num_kept, libmambahip), Int64, (Ptr{Void},), e)
+
+# the one collective (mmb_comm_*): RCCL over xGMI inside the library
+function comm_id()
+  id = zeros(UInt8, MMB_COMM_ID_BYTES)
+  check(ccall((:mmb_comm_id, libmambahip), Cint, (Ptr{UInt8},), id), C_NULL); id
+end
+function comm_init(engines::Vector{Ptr{Void}}, nranks::Integer=length(engines), rank0::Integer=0,
+                   id::Vector{UInt8}=UInt8[])
+  c = Ref{Ptr{Void}}(C_NULL)
+  check(ccall((:mmb_comm_init, libmambahip), Cint,
+              (Ptr{Ptr{Void}}, Cint, Cint, Cint, Ptr{UInt8}, Ref{Ptr{Void}}),
+              engines, length(engines), nranks, rank0, isempty(id) ? C_NULL : pointer(id), c), engines[1])
+  c[]
+end
+comm_destroy(c) = ccall((:mmb_comm_destroy, libmambahip), Void, (Ptr{Void},), c)
+function range_allreduce(c, e, p::Integer)
+  mm = Array{Float64}(2, p)
+  check(ccall((:mmb_range_allreduce, libmambahip), Cint, (Ptr{Void}, Ptr{Float64}), c, mm), e); mm
+end
+function gr_allreduce(c, e, link::Vector{Int32}, shift::Vector{Float64})
+  out = Array{Float64}(gr_len(e))
+  check(ccall((:mmb_gr_allreduce, libmambahip), Cint, (Ptr{Void}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}),
+              c, link, shift, out), e); out
+end
+
+# ---- model lowering --------------------------------------------------------------------------
+# Engine value layout per model kind (include/mamba_hip.h node ids; model.py offsets):
+const LAYOUT = Dict(
+  MMB_MODEL_LINE => [(:beta, 0, 2), (:s2, 1, 1)],                         # doc/tutorial/line.jl:5-25
+  MMB_MODEL_RATS => [(:s2_c, 0, 1), (:alpha, 1, 30), (:mu_alpha, 2, 1), (:s2_alpha, 3, 1),
+                     (:beta, 4, 30), (:mu_beta, 5, 1), (:s2_beta, 6, 1)],  # doc/examples/rats.jl:48-97
+  MMB_MODEL_LOGISTIC => [(:beta, 0, 0)])                                   # SURVEY §8a, p from the node
+
+"A Gibbs block the engine runs natively: `Sampler(params, f, GibbsTune())` with f the
+conjugate full conditional of INTEGRATION.md §3 (the Julia path still calls f)."
+type GibbsTune <: SamplerTune end
+Gibbs(params::Vector{Symbol}, f::Function) = Sampler(params, f, GibbsTune())
+
+function model_kind(m::Model)
+  ks = Set(keys(m, :dependent))                     # Logical + Stochastic nodes (inputs excluded)
+  ks == Set([:y, :beta, :s2, :mu]) && return MMB_MODEL_LINE
+  ks == Set([:y, :alpha, :alpha0, :mu_alpha, :s2_alpha, :beta, :mu_beta, :s2_beta, :s2_c]) &&
+    return MMB_MODEL_RATS
+  ks == Set([:y, :p, :beta]) && return MMB_MODEL_LOGISTIC
+  nothing                                           # (node IR lowering: INTEGRATION.md §2a)
+end
+
+node_id(kind, key::Symbol) = (for (k, id, _) in LAYOUT[kind]; k == key && return id; end; nothing)
+captured(f::Function, name::Symbol, default) = name in fieldnames(typeof(f)) ? getfield(f, name) : default
+function kwarg(f::Function, name::Symbol, default)
+  for (k, v) in captured(f, :args, [])           # AMM(...; beta=, scale=) keyword splat
+    k == name && return v
+  end
+  default
+end
+
+"Model -> (ModelSpec, buffers to keep alive) or nothing (Julia path).  Mirror: model.py Model.spec().
+The sampler kind comes from the type of `s.tune` (created by each constructor, amwg.jl:60,
+amm.jl:58, nuts.jl:55, slice.jl:57, hmc.jl:64, mala.jl:59); constructor arguments are the
+variables the `samplerfx` closure captured (sigma / Sigma / width / pargs / adapt / args)."
+function lower(m::Model)
+  kind = model_kind(m)
+  kind === nothing && return nothing
+  length(m.samplers) > 8 && return nothing
+  blocks = fill(NOBLOCK, 8)
+  keep = Any[]
+  for (b, s) in enumerate(m.samplers)
+    length(s.params) > 4 && return nothing
+    ids = Int32[]
+    for p in s.params
+      id = node_id(kind, p)
+      id === nothing && return nothing
+      push!(ids, id)
+    end
+    nodes = ntuple(i -> i <= length(ids) ? ids[i] : Int32(0), 4)
+    dim = sum(p -> length(m[p].value), s.params)
+    t, f = s.tune, s.eval
+    adapt = MMB_ADAPT[captured(f, :adapt, :none)]
+    blk(kind_, adapt_, form, transform, batchsize, target, beta, scale, tun, eps, L) =
+      BlockSpec(kind_, length(ids), nodes, adapt_, form, transform, batchsize, target, beta, scale, dim,
+                length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L, 0)
+    if isa(t, GibbsTune)
+      sp = blk(MMB_SAMPLER_GIBBS, MMB_ADAPT[:none], 0, 0, 0, 0.0, 0.0, 0.0, Float64[], 0.0, 0)
+    elseif isa(t, AMWGTune)                                                    # amwg.jl:47-61
+      sig = Float64[captured(f, :sigma, 1.0)...]; push!(keep, sig)
+      sp = blk(MMB_SAMPLER_AMWG, adapt, 0, 1, kwarg(f, :batchsize, 50), kwarg(f, :target, 0.44), 0.0, 0.0,
+               sig, 0.0, 0)
+    elseif isa(t, AMMTune)                                                     # amm.jl:45-59
+      Sig = vec(Float64[captured(f, :Sigma, eye(dim))...]); push!(keep, Sig)   # column-major
+      sp = blk(MMB_SAMPLER_AMM, adapt, 0, 1, 0, 0.0, kwarg(f, :beta, 0.05), kwarg(f, :scale, 2.38), Sig, 0.0, 0)
+    elseif isa(t, NUTSTune)                                                    # nuts.jl:47-56
+      sp = blk(MMB_SAMPLER_NUTS, MMB_ADAPT[:burnin], 0, 1, 0, kwarg(f, :target, 0.6), 0.0, 0.0, Float64[], 0.0, 0)
+    elseif isa(t, SliceTune)                                                   # slice.jl:47-58
+      w = Float64[captured(f, :width, 1.0)...]; push!(keep, w)
+      form = isa(t, SliceTune{Univariate}) ? Int32(1) : Int32(0)
+      sp = blk(MMB_SAMPLER_SLICE, MMB_ADAPT[:none], form, Int32(captured(f, :transform, false)), 0, 0.0, 0.0,
+               0.0, w, 0.0, 0)
+    elseif isa(t, HMCTune) || isa(t, MALATune)                                 # hmc.jl:47-65, mala.jl:43-58
+      pargs = captured(f, :pargs, ())                  # (epsilon, L[, Sigma]) / (epsilon[, Sigma])
+      hmc = isa(t, HMCTune)
+      nS = hmc ? 3 : 2
+      S = length(pargs) >= nS ? vec(Float64[pargs[nS]...]) : Float64[]; push!(keep, S)
+      sp = blk(hmc ? MMB_SAMPLER_HMC : MMB_SAMPLER_MALA, MMB_ADAPT[:none], 0, 1, 0, 0.0, 0.0, 0.0, S,
+               Float64(pargs[1]), hmc ? Int32(pargs[2]) : Int32(0))
+    else
+      return nothing                                # an arbitrary user closure: keep the Julia path
+    end
+    blocks[b] = sp
+  end
+  nobs = kind == MMB_MODEL_LOGISTIC ? length(m[:y].value) : 0
+  ncoef = kind == MMB_MODEL_LOGISTIC ? length(m[:beta].value) : 0
+  prior_sd = kind == MMB_MODEL_LOGISTIC ? sqrt(m[:beta].distr.Σ.value) : 0.0
+  (ModelSpec(kind, length(m.samplers), tuple(blocks...), nobs, ncoef, prior_sd, ntuple(_ -> Int32(0), 8)), keep)
+end
+
+"setinputs! data the kernels read (names of include/mamba_hip.h mmb_set_data)."
+function inputs(m::Model, kind)
+  kind == MMB_MODEL_LINE && return [("x", Float64[m[:x].value...]), ("y", Float64[m[:y].value...])]
+  kind == MMB_MODEL_RATS && return [("y", Float64[m[:y].value...]), ("x", Float64[m[:x].value...])]
+  [("X", vec(full(m[:X].value)')), ("y", Float64[m[:y].value...])]                # X row-major
+end
+
+"One chain's values in the engine layout (P), after relist!(m, state.value) (mcmc.jl:68-70)."
+function engine_values(m::Model, kind)
+  vcat([Float64[m[k].value...] for (k, _, _) in LAYOUT[kind]]...)
+end
+function set_engine_values!(m::Model, kind, v::AbstractVector{Float64})
+  o = 0
+  for (k, _, _) in LAYOUT[kind]
+    n = length(m[k].value)
+    m[k].value = n == 1 && isa(m[k].value, Real) ? v[o + 1] : reshape(v[o + (1:n)], size(m[k].value))
+    o += n
+  end
+end
+
+# ---- tune <-> canonical engine tune row (engine.cpp mmb_get_tune / mmb_set_tune) -------------
+tri(i) = div(i * (i + 1), 2)                        # 0-based packed-lower helpers (device.h)
+slot(i, k) = i >= k ? tri(i) + k : tri(k) + i
+
+"Canonical tune row of block b for one chain from its Julia tune object."
+function pack_tune(t, s::Sampler, dim::Integer, iter::Integer)
+  if isa(t, AMWGTune)                               # [adapt, m, sigma[d], accept[d]]
+    return vcat(Float64(t.adapt), Float64(t.m), t.sigma, Float64[t.accept...])
+  elseif isa(t, AMMTune)                            # [adapt, m, valid, alias, Mv, Mvv, Ls, piv]
+    T = tri(dim)
+    Mv = isempty(t.Mv) ? zeros(dim) : Float64[t.Mv...]
+    Mvv, Ls, piv = zeros(T), zeros(T), zeros(dim)
+    if !isempty(t.Mvv)
+      for i in 0:dim-1, k in 0:i; Mvv[tri(i) + k + 1] = t.Mvv[k + 1, i + 1]; end     # upper semantics
+    end
+    valid = !isempty(t.SigmaLm) && any(x -> x != 0.0, t.SigmaLm)
+    if valid                                        # SigmaLm = P*L: row e's last nonzero = pos(e)
+      pos = [findlast(x -> x != 0.0, t.SigmaLm[e + 1, :]) - 1 for e in 0:dim-1]
+      for e in 0:dim-1; piv[pos[e + 1] + 1] = e; end
+      for e in 0:dim-1
+        for k in 0:pos[e + 1]-1; Ls[slot(e, Int(piv[k + 1])) + 1] = t.SigmaLm[e + 1, k + 1]; end
+        Ls[slot(e, e) + 1] = t.SigmaLm[e + 1, pos[e + 1] + 1]
+      end
+    end
+    return vcat(Float64(t.adapt), Float64(t.m), Float64(valid), 0.0, Mv, Mvv, Ls, piv)
+  elseif isa(t, NUTSTune)                           # [adapt, m, eps, epsbar, Hbar, mu, alpha, nalpha, init]
+    return Float64[t.adapt, t.m, t.epsilon, t.epsbar, t.Hbar, t.mu, t.alpha, t.nalpha, iter >= 1]
+  elseif isa(t, HMCTune)
+    return Float64[t.epsilon, t.L]
+  elseif isa(t, MALATune)
+    return Float64[t.epsilon]
+  end
+  Float64[]                                         # Slice, Gibbs: nothing is adapted
+end
+
+"Inverse of pack_tune: write one chain's canonical row back into its Julia tune object."
+function unpack_tune!(t, row::AbstractVector{Float64}, dim::Integer)
+  if isa(t, AMWGTune)
+    t.adapt = row[1] != 0; t.m = Int(row[2])
+    t.sigma = row[3:2+dim]; t.accept = Int[row[3+dim:2+2dim]...]
+  elseif isa(t, AMMTune)
+    T = tri(dim)
+    t.adapt = row[1] != 0; t.m = Int(row[2])
+    t.Mv = row[5:4+dim]
+    Mvv = zeros(dim, dim)
+    for i in 0:dim-1, k in 0:i; Mvv[k + 1, i + 1] = Mvv[i + 1, k + 1] = row[5 + dim + tri(i) + k]; end
+    t.Mvv = Mvv
+    if row[3] != 0
+      Ls = row[5+dim+T:4+dim+2T]; piv = Int[row[5+dim+2T:4+2dim+2T]...]
+      pos = zeros(Int, dim); for k in 0:dim-1; pos[piv[k + 1] + 1] = k; end
+      S = zeros(dim, dim)
+      for e in 0:dim-1
+        for k in 0:pos[e + 1]-1; S[e + 1, k + 1] = Ls[slot(e, piv[k + 1]) + 1]; end
+        S[e + 1, pos[e + 1] + 1] = Ls[slot(e, e) + 1]
+      end
+      t.SigmaLm = S
+    else
+      t.SigmaLm = zeros(dim, dim)
+    end
+  elseif isa(t, NUTSTune)
+    t.adapt = row[1] != 0; t.m = Int(row[2]); t.epsilon, t.epsbar, t.Hbar, t.mu, t.alpha = row[3:7]
+    t.nalpha = Int(row[8])
+  elseif isa(t, HMCTune)
+    t.epsilon, t.L = row[1], Int(row[2])
+  elseif isa(t, MALATune)
+    t.epsilon = row[1]
+  end
+  t
+end
+
+"K x TL canonical tune (column = chain) from the per-chain ModelStates."
+function pack_tunes(m::Model, states::Vector{ModelState}, iter::Integer)
+  cols = Vector{Float64}[]
+  for st in states
+    row = Float64[]
+    for (b, s) in enumerate(m.samplers)
+      dim = sum(p -> length(m[p].value), s.params)
+      append!(row, pack_tune(st.tune[b], s, dim, iter))
+    end
+    push!(cols, row)
+  end
+  hcat(cols...)
+end
+
+"m.states[k] = ModelState(values, tune) from the engine after a window (mcmc.jl:54-56, 82)."
+function store_states!(m::Model, e, kind, states::Vector{ModelState})
+  K = length(states)
+  vals = Array{Float64}(num_values(e), K); get_values!(e, vals)
+  TL = tune_len(e)
+  tunes = Array{Float64}(TL, K)
+  TL > 0 && get_tune!(e, tunes)
+  for k in 1:K
+    set_engine_values!(m, kind, vals[:, k])
+    tune = deepcopy(states[k].tune)
+    o = 0
+    for (b, s) in enumerate(m.samplers)
+      dim = sum(p -> length(m[p].value), s.params)
+      n = length(pack_tune(tune[b], s, dim, 1))
+      unpack_tune!(tune[b], tunes[o + 1:o + n, k], dim)
+      o += n
+    end
+    states[k] = ModelState(unlist(m), tune)
+  end
+  m.states = states
+end
+
+# ---- the mcmc_master! branch (src/model/mcmc.jl:36-59) ----------------------------------------
+"""
+    run_chains!(m, window, burnin, thin, chains; device=0, seed=...) -> ModelChains or nothing
+
+The GPU path of `mcmc_master!`: `nothing` when `lower(m)` does not recognise the model or a
+block (the caller then runs `pmap2(mcmc_worker!, lsts)` unchanged).  Global chain id of
+chains[k] is chains[k] - 1, so a chain's Philox streams (and its draws) do not depend on
+how chains are split over calls or GPUs.
+"""
+function run_chains!(m::Model, window::UnitRange{Int}, burnin::Integer, thin::Integer,
+                     chains::AbstractArray{Int}; device::Integer=0, seed::UInt64=UInt64(20261015))
+  low = lower(m)
+  low === nothing && return nothing
+  spec, keep = low
+  kind = spec.model
+  e = create(spec, device)
+  e === nothing && return nothing
+  try
+    for (name, x) in inputs(m, kind); set_data!(e, name, x); end
+    states = m.states
+    init = hcat([(relist!(m, st.value); engine_values(m, kind)) for st in states]...)   # P x K
+    offset = first(chains) - 1
+    chains == offset + (1:length(chains)) || throw(ArgumentError("chains must be a contiguous range"))
+    init_chains!(e, init, offset, seed)
+    first(window) > 1 && set_tune!(e, pack_tunes(m, states, first(window) - 1))        # restart
+    set_iter!(e, first(window) - 1)
+    K = length(chains)
+    nkept = length(filter(i -> i > burnin && (i - burnin) % thin == 0, window))
+    names = Mamba.names(m, true)
+    sim = Chains(nkept, length(names), chains=K, start=first(filter(i -> i > burnin && (i - burnin) % thin == 0,
+                                                                     window)), thin=thin, names=names)
+    a = RunArgs(length(window), burnin, thin, m.burnin, pointer(sim.value), 0, 0)
+    run!(e, a)                                         # writes n x p x K in Chains order
+    store_states!(m, e, kind, states)
+    m.iter = last(window)
+    return ModelChains(sim, m)
+  finally
+    destroy(e)
+    keep = nothing
+  end
+end
+
+# In src/model/mcmc.jl, first lines of mcmc_master!:
+#   if haskey(ENV, "MAMBA_HIP")
+#     mc = MambaHIP.run_chains!(m, window, burnin, thin, chains; device=gpu_device())
+#     mc === nothing || return mc
+#   end
+
+"""
+    gelmandiag(engines, p; nranks, rank, id) -> psrf sums (mmb_gr_len doubles)
+
+Cross-GPU sufficient statistics of gelmandiag (gelmandiag.jl:11-25) through the library's own
+RCCL communicator; the PSRF follows as in Mamba's gelmandiag (mirror: gelman.py psrf_from_sums).
+"""
+function gelmandiag_sums(engines::Vector{Ptr{Void}}, p::Integer; nranks::Integer=length(engines),
+                         rank0::Integer=0, id::Vector{UInt8}=UInt8[])
+  c = comm_init(engines, nranks, rank0, id)
+  try
+    mm = range_allreduce(c, engines[1], p)
+    shift = vec(0.5 * (mm[1, :] + mm[2, :]))
+    return gr_allreduce(c, engines[1], zeros(Int32, p), shift)
+  finally
+    comm_destroy(c)
+  end
+end
+
+end # module

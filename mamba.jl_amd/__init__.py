@@ -8,7 +8,7 @@ The package directory is `mamba.jl_amd/`; import it as `mamba_amd` via
 `_mamba_path.load()` (the dot in the directory name is not importable directly).
 """
 from . import abi, gelman, ir, model, samplers, summary  # noqa: F401
-from .gelman import gelmandiag, gelmandiag_sharded, psrf_from_sums  # noqa: F401
+from .gelman import Comm, gelmandiag, gelmandiag_rccl, gelmandiag_sharded, psrf_from_sums  # noqa: F401
 from .summary import pool_summary, quantile_sharded, summarystats_sharded  # noqa: F401
 from .mcmc import Chains, Engine, mcmc, mcmc_restart, read, write  # noqa: F401
 from .model import line, logistic, rats  # noqa: F401

@@ -13,7 +13,7 @@ MMB_MAX_NODES_PER_BLOCK = 4
 MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC, MMB_MODEL_IR = 1, 2, 3, 4
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
-MMB_ABI_VERSION = 3
+MMB_ABI_VERSION = 4
 MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
 MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
@@ -31,7 +31,8 @@ IR_OP = {"end": 0, "const": 1, "val": 2, "vali": 3, "valg": 4, "data": 5, "datas
 MMB_IR_MAX_STACK, MMB_IR_MAX_TERMS, MMB_IR_MAX_VALUES = 16, 16, 512
 
 ERRORS = {-1: "invalid argument", -2: "unsupported model/scheme", -3: "HIP runtime error",
-          -4: "call out of order", -5: "out of memory"}
+          -4: "call out of order", -5: "out of memory", -6: "RCCL error"}
+MMB_COMM_ID_BYTES = 128
 
 
 class BlockSpec(C.Structure):
@@ -110,6 +111,11 @@ def _declare(lib):
         "mmb_state_bytes": (C.c_int, [P, D]),
         "mmb_grad_evals": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_nuts_stats": (C.c_int, [P, C.POINTER(I64)]),
+        "mmb_comm_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+        "mmb_comm_init": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(P)]),
+        "mmb_range_allreduce": (C.c_int, [P, D]),
+        "mmb_gr_allreduce": (C.c_int, [P, C.POINTER(I32), D, D]),
+        "mmb_comm_destroy": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -21,6 +21,8 @@
 #include "logistic.h"
 #include "ir.h"
 
+#include <rccl/rccl.h>
+
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st);
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st);
@@ -1216,7 +1218,12 @@ int mmb_gr_partials(mmb_engine* e, const int32_t* link, const double* shift, dou
   HIPCHK(e, hipMemcpyAsync(dl, link, p * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
   HIPCHK(e, hipMemcpyAsync(ds, shift, p * sizeof(double), hipMemcpyHostToDevice, e->stream));
   hipError_t st = mmb_launch_gr_stats(p, e->n_kept, (int)e->K, e->d_draws, dl, ds, dout, e->stream);
-  if (st != hipSuccess) return fail(e, MMB_E_HIP, "gr_stats: %s", hipGetErrorString(st));
+  if (st != hipSuccess) {
+    (void)hipFree(dl);
+    (void)hipFree(ds);
+    (void)hipFree(dout);
+    return fail(e, MMB_E_HIP, "gr_stats: %s", hipGetErrorString(st));
+  }
   HIPCHK(e, hipMemcpyAsync(out, dout, L * sizeof(double), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   (void)hipFree(dl);
@@ -1331,4 +1338,159 @@ int mmb_grad_evals(mmb_engine* e, int64_t* n) {
   HIPCHK(e, hipStreamSynchronize(e->stream));
   *n = (int64_t)v;
   return 0;
+}
+
+// ---------------------------------------------------------------- cross-GPU Gelman-Rubin (RCCL)
+// The one collective of the path (gelmandiag.jl:11-25): each local engine reduces
+// its kept draws to the mmb_gr_len sufficient statistics on device (gr.hip), then one SUM
+// all-reduce over RCCL/xGMI, in place in a per-engine device buffer; the global [min, max]
+// used for link() and the shift is one MAX all-reduce of (-min, max).
+struct mmb_comm {
+  std::vector<mmb_engine*> eng;
+  std::vector<ncclComm_t> comm;
+  std::vector<double*> buf;  // per local engine: [L stats | 2p range | p shift | p link (int32)]
+  int p = 0;
+  int64_t L = 0;
+};
+
+#define NCCLCHK(e, x)                                                                 \
+  do {                                                                                \
+    ncclResult_t r_ = (x);                                                            \
+    if (r_ != ncclSuccess) return fail((e), MMB_E_COMM, "%s: %s", #x, ncclGetErrorString(r_)); \
+  } while (0)
+
+__global__ void mmb_negate_mins(double* mm, int p) {
+  const int j = (int)threadIdx.x;
+  if (j < p) mm[2 * j] = -mm[2 * j];
+}
+
+int mmb_comm_id(uint8_t* id) {
+  if (!id) return fail(nullptr, MMB_E_ARG, "null argument");
+  ncclUniqueId u;
+  NCCLCHK(nullptr, ncclGetUniqueId(&u));
+  std::memcpy(id, u.internal, MMB_COMM_ID_BYTES);
+  return 0;
+}
+
+void mmb_comm_destroy(mmb_comm* c) {
+  if (!c) return;
+  for (size_t i = 0; i < c->eng.size(); ++i) {
+    (void)hipSetDevice(c->eng[i]->device);
+    if (c->comm[i]) (void)ncclCommDestroy(c->comm[i]);
+    if (c->buf[i]) (void)hipFree(c->buf[i]);
+  }
+  delete c;
+}
+
+int mmb_comm_init(mmb_engine** engines, int nlocal, int nranks, int rank0, const uint8_t* id, mmb_comm** out) {
+  if (!engines || !out || nlocal < 1) return fail(nullptr, MMB_E_ARG, "null argument or nlocal < 1");
+  *out = nullptr;
+  mmb_engine* e0 = engines[0];
+  if (!e0) return fail(nullptr, MMB_E_ARG, "null engine");
+  if (nranks < nlocal || rank0 < 0 || rank0 + nlocal > nranks)
+    return fail(e0, MMB_E_ARG, "ranks %d..%d outside 0..%d", rank0, rank0 + nlocal - 1, nranks - 1);
+  if (nlocal < nranks && !id) return fail(e0, MMB_E_ARG, "ranks span processes: pass the mmb_comm_id bytes of rank 0");
+  for (int i = 0; i < nlocal; ++i) {
+    if (!engines[i]) return fail(e0, MMB_E_ARG, "null engine %d", i);
+    if (engines[i]->pmon != e0->pmon) return fail(e0, MMB_E_ARG, "engines monitor different parameter counts");
+    for (int k = 0; k < i; ++k)
+      if (engines[k]->device == engines[i]->device) return fail(e0, MMB_E_ARG, "two local engines on device %d", engines[i]->device);
+  }
+  mmb_comm* c = new mmb_comm;
+  c->eng.assign(engines, engines + nlocal);
+  c->comm.assign(nlocal, nullptr);
+  c->buf.assign(nlocal, nullptr);
+  c->p = e0->pmon;
+  c->L = mmb_gr_len(e0);
+  const size_t nbuf = (size_t)c->L + 4 * (size_t)c->p;
+  for (int i = 0; i < nlocal; ++i) {
+    if (hipSetDevice(engines[i]->device) != hipSuccess || hipMalloc(&c->buf[i], nbuf * sizeof(double)) != hipSuccess) {
+      mmb_comm_destroy(c);
+      return fail(e0, MMB_E_HIP, "comm buffer allocation failed");
+    }
+  }
+  ncclResult_t r;
+  if (nlocal == nranks && !id) {
+    std::vector<int> devs(nlocal);
+    for (int i = 0; i < nlocal; ++i) devs[i] = engines[i]->device;
+    r = ncclCommInitAll(c->comm.data(), nlocal, devs.data());
+  } else {
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, MMB_COMM_ID_BYTES);
+    r = ncclGroupStart();
+    for (int i = 0; r == ncclSuccess && i < nlocal; ++i) {
+      (void)hipSetDevice(engines[i]->device);
+      r = ncclCommInitRank(&c->comm[i], nranks, u, rank0 + i);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+  }
+  if (r != ncclSuccess) {
+    mmb_comm_destroy(c);
+    return fail(e0, MMB_E_COMM, "RCCL communicator init (%d local of %d ranks): %s", nlocal, nranks,
+                ncclGetErrorString(r));
+  }
+  *out = c;
+  return 0;
+}
+
+static int comm_sync(mmb_comm* c) {
+  for (mmb_engine* e : c->eng) {
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  return 0;
+}
+
+int mmb_range_allreduce(mmb_comm* c, double* minmax) {
+  if (!c || !minmax) return fail(nullptr, MMB_E_ARG, "null argument");
+  mmb_engine* e0 = c->eng[0];
+  const int p = c->p;
+  for (size_t i = 0; i < c->eng.size(); ++i) {
+    mmb_engine* e = c->eng[i];
+    if (e->n_kept < 1) return fail(e0, MMB_E_STATE, "no device-kept draws on engine %zu", i);
+    HIPCHK(e0, hipSetDevice(e->device));
+    double* mm = c->buf[i] + c->L;
+    hipError_t st = mmb_launch_gr_range(p, e->n_kept, (int)e->K, e->d_draws, mm, e->stream);
+    if (st != hipSuccess) return fail(e0, MMB_E_HIP, "gr_range: %s", hipGetErrorString(st));
+    hipLaunchKernelGGL(mmb_negate_mins, dim3(1), dim3(((p + 63) / 64) * 64), 0, e->stream, mm, p);
+    HIPCHK(e0, hipGetLastError());
+  }
+  NCCLCHK(e0, ncclGroupStart());
+  for (size_t i = 0; i < c->eng.size(); ++i) {
+    double* mm = c->buf[i] + c->L;
+    NCCLCHK(e0, ncclAllReduce(mm, mm, 2 * (size_t)p, ncclDouble, ncclMax, c->comm[i], c->eng[i]->stream));
+  }
+  NCCLCHK(e0, ncclGroupEnd());
+  HIPCHK(e0, hipSetDevice(e0->device));
+  HIPCHK(e0, hipMemcpyAsync(minmax, c->buf[0] + c->L, 2 * p * sizeof(double), hipMemcpyDeviceToHost, e0->stream));
+  int rc = comm_sync(c);
+  if (rc) return rc;
+  for (int j = 0; j < p; ++j) minmax[2 * j] = -minmax[2 * j];
+  return 0;
+}
+
+int mmb_gr_allreduce(mmb_comm* c, const int32_t* link, const double* shift, double* out) {
+  if (!c || !link || !shift || !out) return fail(nullptr, MMB_E_ARG, "null argument");
+  mmb_engine* e0 = c->eng[0];
+  const int p = c->p;
+  for (size_t i = 0; i < c->eng.size(); ++i) {
+    mmb_engine* e = c->eng[i];
+    if (e->n_kept < 2) return fail(e0, MMB_E_STATE, "need >= 2 device-kept draws per chain (engine %zu)", i);
+    HIPCHK(e0, hipSetDevice(e->device));
+    double* ds = c->buf[i] + c->L + 2 * p;
+    int32_t* dl = (int32_t*)(ds + p);
+    HIPCHK(e0, hipMemcpyAsync(ds, shift, p * sizeof(double), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e0, hipMemcpyAsync(dl, link, p * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+    hipError_t st = mmb_launch_gr_stats(p, e->n_kept, (int)e->K, e->d_draws, dl, ds, c->buf[i], e->stream);
+    if (st != hipSuccess) return fail(e0, MMB_E_HIP, "gr_stats: %s", hipGetErrorString(st));
+  }
+  NCCLCHK(e0, ncclGroupStart());
+  for (size_t i = 0; i < c->eng.size(); ++i)
+    NCCLCHK(e0, ncclAllReduce(c->buf[i], c->buf[i], (size_t)c->L, ncclDouble, ncclSum, c->comm[i], c->eng[i]->stream));
+  NCCLCHK(e0, ncclGroupEnd());
+  HIPCHK(e0, hipSetDevice(e0->device));
+  HIPCHK(e0, hipMemcpyAsync(out, c->buf[0], c->L * sizeof(double), hipMemcpyDeviceToHost, e0->stream));
+  // the host copies of link/shift must outlive the async H2D copies: wait before returning
+  return comm_sync(c);
 }

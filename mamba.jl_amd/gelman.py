@@ -8,8 +8,12 @@ sums into the PSRF / upper limit / MPSRF exactly as gelmandiag.jl does.
 L-vector layout for p monitored params (phi = chain mean - shift):
   [m, sum phi (p), sum phi phi' (p*p), sum S2 (p*p), sum s2^2 (p), sum s2*phi (p), sum s2*phi^2 (p)]
 """
+import ctypes as C
+
 import numpy as np
 from scipy import stats
+
+from . import abi
 
 
 def link_kinds(minmax):
@@ -109,3 +113,75 @@ def gelmandiag(chains, alpha=0.05, mpsrf=False, transform=False):
     sums = np.concatenate([[m], phi.sum(0), (phi.T @ phi).ravel(), S2.sum(2).ravel(),
                            (s2**2).sum(0), (s2 * phi).sum(0), (s2 * phi**2).sum(0)])
     return psrf_from_sums(sums, n, p, alpha=alpha, mpsrf=mpsrf)
+
+
+class Comm:
+    """The library's own RCCL communicator (include/mamba_hip.h mmb_comm_*): the one
+    cross-GPU collective of the path, reachable from any C caller.
+
+    Comm([e0, e1, ...])                       one process driving all its GPUs (ncclCommInitAll)
+    Comm([e], nranks=N, rank0=r, uid=bytes)   one process per GPU; rank 0 makes `uid` with
+                                              Comm.unique_id() and the caller broadcasts it
+    """
+
+    def __init__(self, engines, nranks=None, rank0=0, uid=None):
+        self.lib = abi.lib()
+        self.engines = list(engines)
+        n = len(self.engines)
+        nranks = n if nranks is None else int(nranks)
+        arr = (C.c_void_p * n)(*[e.h for e in self.engines])
+        idp = None
+        if uid is not None:
+            if len(uid) != abi.MMB_COMM_ID_BYTES:
+                raise ValueError(f"unique id must be {abi.MMB_COMM_ID_BYTES} bytes")
+            idp = (C.c_uint8 * abi.MMB_COMM_ID_BYTES)(*uid)
+        h = C.c_void_p()
+        abi.check(self.lib.mmb_comm_init(arr, n, nranks, int(rank0), idp, C.byref(h)), self.engines[0].h)
+        self.h = h
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * abi.MMB_COMM_ID_BYTES)()
+        abi.check(abi.lib().mmb_comm_id(buf))
+        return bytes(buf)
+
+    def range_allreduce(self):
+        """Global [min, max] per monitored param over every chain of every rank (p x 2)."""
+        p = self.engines[0].pmon
+        out = np.empty(2 * p)
+        abi.check(self.lib.mmb_range_allreduce(self.h, abi.dptr(out)), self.engines[0].h)
+        return out.reshape(p, 2)
+
+    def gr_allreduce(self, kinds, shift):
+        """Global Gelman-Rubin sufficient statistics (mmb_gr_len doubles)."""
+        kinds = np.ascontiguousarray(kinds, dtype=np.int32)
+        shift = np.ascontiguousarray(shift, dtype=np.float64)
+        out = np.empty(self.lib.mmb_gr_len(self.engines[0].h))
+        abi.check(self.lib.mmb_gr_allreduce(self.h, kinds.ctypes.data_as(C.POINTER(C.c_int32)), abi.dptr(shift),
+                                            abi.dptr(out)), self.engines[0].h)
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mmb_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gelmandiag_rccl(comm, transform=False, alpha=0.05, mpsrf=False):
+    """gelmandiag over every chain of every rank of `comm`, all reductions inside the
+    library (RCCL): one MAX all-reduce for the range, one SUM all-reduce of the sums."""
+    eng = comm.engines[0]
+    mm = comm.range_allreduce()
+    kinds = link_kinds(mm) if transform else np.zeros(eng.pmon, dtype=np.int32)
+    mid = 0.5 * (mm[:, 0] + mm[:, 1])
+    shift = mid.copy()
+    shift[kinds == 1] = np.log(mid[kinds == 1])
+    shift[kinds == 2] = np.log(mid[kinds == 2] / (1.0 - mid[kinds == 2]))
+    tot = comm.gr_allreduce(kinds, shift)
+    return psrf_from_sums(tot, eng.num_kept(), eng.pmon, alpha=alpha, mpsrf=mpsrf)

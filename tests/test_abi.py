@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(mamba):
     assert len(syms) >= 20
     missing = [s for s in syms if s not in exported]
     assert not missing, missing
-    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 3
+    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 4
 
 
 def test_struct_layout_matches_header(mamba):
@@ -115,3 +115,16 @@ def test_chains_file_round_trip(mamba, tmp_path):
     np.savez(bad, value=val)
     with pytest.raises(TypeError):
         mamba.read(bad)
+
+
+def test_comm_init_validates_before_touching_the_device(mamba):
+    """mmb_comm_init rejects bad rank layouts on the host (no GPU, no RCCL call here)."""
+    lib = mamba.abi.lib()
+    h = C.c_void_p()
+    assert lib.mmb_comm_init(None, 1, 1, 0, None, C.byref(h)) == -1
+    arr = (C.c_void_p * 1)(None)
+    assert lib.mmb_comm_init(arr, 0, 1, 0, None, C.byref(h)) == -1
+    assert lib.mmb_comm_init(arr, 1, 1, 0, None, C.byref(h)) == -1          # null engine
+    assert lib.mmb_range_allreduce(None, None) == -1
+    assert lib.mmb_gr_allreduce(None, None, None, None) == -1
+    lib.mmb_comm_destroy(None)

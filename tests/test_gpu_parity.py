@@ -426,3 +426,28 @@ def test_slice_shrink_overflow_is_an_error(mamba, form):
     e2 = mamba.Engine(m2)
     e2.init_chains(mamba.model.line_init_matrix(3, seed=1), seed=2)
     assert np.isfinite(e2.run(5, burnin=0, thin=1)).all()
+
+
+@pytest.mark.parametrize("how", ["init_all", "unique_id"])
+def test_gr_allreduce_rccl_one_gpu(mamba, how):
+    """mmb_comm_init + mmb_range_allreduce + mmb_gr_allreduce (gelmandiag.jl:11-25)
+    at ngpu = 1, through both communicator forms (ncclCommInitAll; ncclCommInitRank with a
+    unique id): the RCCL sums equal the engine's own partials bit for bit (a one-rank SUM is
+    the identity) and the PSRF equals the host gelmandiag of the same draws."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(512, seed=3), seed=4)
+    d = eng.run(240, burnin=40, thin=2, keep_device=True)
+    comm = (mamba.Comm([eng]) if how == "init_all"
+            else mamba.Comm([eng], nranks=1, rank0=0, uid=mamba.Comm.unique_id()))
+    mm = comm.range_allreduce()
+    np.testing.assert_array_equal(mm, eng.gr_range())
+    for transform in (False, True):
+        ps, mp = mamba.gelmandiag_rccl(comm, transform=transform, mpsrf=True)
+        ps_h, mp_h = mamba.gelmandiag(d, transform=transform, mpsrf=True)
+        np.testing.assert_allclose(ps, ps_h, rtol=1e-8)
+        assert mp == pytest.approx(mp_h, rel=1e-8)
+    kinds = np.array([1, 0, 0], dtype=np.int32)
+    shift = np.array([3.6, 6.0, 100.0])
+    np.testing.assert_array_equal(comm.gr_allreduce(kinds, shift), eng.gr_partials(kinds, shift))
+    comm.close()
