@@ -296,12 +296,22 @@ def main():
     # MMB_DIST_BACKEND=gloo (several ranks sharing one GPU, which RCCL refuses) reduces the same
     # device partials through torch.distributed on the host instead.
     if backend == "nccl":
-        uid = [mb.Comm.unique_id() if rank == 0 else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        comm = mb.Comm([eng], nranks=world, rank0=rank, uid=uid[0])
-        psrf, _ = mb.gelmandiag_rccl(comm)
-        comm.close()
+        # RCCL prints a version banner on stdout at communicator init: keep stdout for the one
+        # JSON line (the banner goes to stderr)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            uid = [mb.Comm.unique_id() if rank == 0 else None]
+            if world > 1:
+                dist.broadcast_object_list(uid, src=0)
+            comm = mb.Comm([eng], nranks=world, rank0=rank, uid=uid[0])
+            psrf, _ = mb.gelmandiag_rccl(comm)
+            comm.close()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         def ar_sum(x):
             t = torch.tensor(x, dtype=torch.float64, device=coll_dev)

@@ -64,6 +64,9 @@ struct DBlock {
   double* t_Mvv;         // AMM   [K][TP] packed lower, row-major (slot(i,k) = i(i+1)/2 + k)
   double* t_Ls;          // AMM   [K][TP] factor, in-place slot storage
   uint8_t* t_piv;        // AMM   [K][DP] pivot order
+  double* t_xnext;       // AMM   [K][DP] next iteration's proposal minus v (samplers.h amm: formed
+                         //       with the factor still in registers), valid when t_xtag[c] matches
+  int64_t* t_xtag;       // AMM   [K] (xepoch << 32) | iteration the carried proposal is for
   double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
   double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
   double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)
@@ -81,6 +84,7 @@ struct SweepArgs {
   int64_t kept_base;     // kept rows before this launch (within the mmb_run window)
   int64_t kept_origin;   // kept count at the window start (rows are relative to the window)
   double* vals;          // model-specific device layout
+  int64_t xepoch;        // bumped by every host write of chain state (invalidates carried proposals)
   unsigned long long* nuts_stat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat),
                                   // [3] Slice updates stopped at MMB_SLICE_MAX_SHRINK
   double* draws;         // [n_kept][pmon][K] or null

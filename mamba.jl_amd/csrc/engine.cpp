@@ -49,6 +49,8 @@ struct BlockHost {
   double* hmc = nullptr;  // HMC/MALA [K][2] epsilon, L
   int32_t *m = nullptr, *flags = nullptr;
   uint8_t* piv = nullptr;
+  double* xnext = nullptr;   // AMM carried next proposal [K][DP] (samplers.h amm)
+  int64_t* xtag = nullptr;   // AMM [K] tag of the carried proposal
 };
 
 struct mmb_engine {
@@ -81,6 +83,7 @@ struct mmb_engine {
   unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum}, Slice overflows
                                           // since init_chains
   unsigned long long slice_overflows = 0;  // d_nstat[3] as last reported by mmb_run
+  int64_t xepoch = 0;  // bumped by every host write of chain state: invalidates carried AMM proposals
   // draws of the last window
   double* d_draws = nullptr;
   size_t draws_cap = 0;
@@ -483,12 +486,14 @@ int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device
 static void free_dev(mmb_engine* e) {
   for (auto& h : e->blocks) {
     void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.nfr, h.width, h.sigl_d, h.hmc, h.m, h.flags,
-                    h.piv};
+                    h.piv, h.xnext, h.xtag};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
     h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.nfr = h.width = h.sigl_d = h.hmc = nullptr;
     h.m = h.flags = nullptr;
     h.piv = nullptr;
+    h.xnext = nullptr;
+    h.xtag = nullptr;
   }
   if (e->d_vals) (void)hipFree(e->d_vals);
   if (e->d_blocks) (void)hipFree(e->d_blocks);
@@ -605,6 +610,7 @@ int mmb_set_iter(mmb_engine* e, int64_t iter) {
   if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
   if (iter < 0 || iter > 0xffffffffLL) return fail(e, MMB_E_ARG, "iteration out of range");
   e->iter = iter;
+  ++e->xepoch;
   return 0;
 }
 int64_t mmb_num_kept(const mmb_engine* e) { return e ? e->n_kept : MMB_E_ARG; }
@@ -643,6 +649,7 @@ static void from_device_layout(const mmb_engine* e, const double* dv, double* v)
 int mmb_set_values(mmb_engine* e, const double* values) {
   if (!e || !values) return fail(e, MMB_E_ARG, "null argument");
   if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  ++e->xepoch;
   std::vector<double> h((size_t)e->K * e->VS);
   for (int64_t k = 0; k < e->K; ++k) to_device_layout(e, values + k * e->P, h.data() + k * e->VS);
   HIPCHK(e, hipSetDevice(e->device));
@@ -694,7 +701,7 @@ static int upload_blocks(mmb_engine* e) {
     d.width = (h.spec.sampler == MMB_SAMPLER_SLICE && h.tuning.size() > 1) ? h.width : nullptr;
     d.sigl = h.sigl_d;
     d.t_sigma = h.sigma; d.t_accept = h.accept; d.t_m = h.m; d.t_flags = h.flags;
-    d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_nuts = h.nuts; d.t_nfr = h.nfr;
+    d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_xnext = h.xnext; d.t_xtag = h.xtag; d.t_nuts = h.nuts; d.t_nfr = h.nfr;
     d.t_hmc = h.hmc;
     d.ir_blk = (int32_t)b;
   }
@@ -752,6 +759,9 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
       for (int64_t k = 0; k < K; ++k)
         for (size_t i = 0; i < DP; ++i) pv[k * DP + i] = (uint8_t)i;
       HIPCHK(e, hipMemcpy(h.piv, pv.data(), pv.size(), hipMemcpyHostToDevice));
+      HIPCHK(e, dalloc(&h.xnext, K * DP));
+      HIPCHK(e, dalloc(&h.xtag, K));
+      HIPCHK(e, hipMemset(h.xtag, 0xff, K * sizeof(int64_t)));  // -1: no carried proposal
       HIPCHK(e, dalloc(&h.sigl_d, (size_t)h.d * h.d));
       HIPCHK(e, hipMemcpy(h.sigl_d, h.sigl.data(), h.sigl.size() * sizeof(double), hipMemcpyHostToDevice));
     } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
@@ -809,6 +819,7 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.seed = e->seed;
   A.nb = (int32_t)e->blocks.size();
   A.vals = e->d_vals;
+  A.xepoch = e->xepoch;
   A.nuts_stat = e->d_nstat;
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
@@ -1123,6 +1134,7 @@ int mmb_get_tune(mmb_engine* e, double* tune) {
 int mmb_set_tune(mmb_engine* e, const double* tune) {
   if (!e || !tune) return fail(e, MMB_E_ARG, "null argument");
   if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  ++e->xepoch;
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   const int64_t TL = mmb_tune_len(e), K = e->K;

@@ -369,7 +369,14 @@ struct Smp {
   //   and NaN candidates go to pivot_exact (dpstf2's first maximum in position order).
   // Measured (rats sweep, 16384 chains): 0.255 -> 0.248 ms; the factorization is bound by
   // its f64 work per step (sqrt, reciprocal, dot product), not by the pivot search.
-  __device__ __forceinline__ static int pchol32(int d, double* mat, double* prow, int* pks, const Grp<G>& g) {
+  // rn1 != null: also returns in *ynext this lane's row of SigmaLm z2' for the next
+  // iteration (z2' = the second normal of each element's pair from rn1), formed from the
+  // factor rows still in registers: P L z2' (amm.jl:74), row e = sum_k L[pos e][k] z2'[k],
+  // k ascending -- the order of the direct matvec in amm().
+  __device__ __forceinline__ static int pchol32(int d, double* mat, double* prow, int* pks, const Grp<G>& g,
+                                                const DBlock* NB = nullptr, const SweepArgs& A = SweepArgs{},
+                                                int c = 0, uint32_t chain = 0, int64_t it = 0, int b = 0,
+                                                int m = 0) {
     constexpr int RI = DMAX;  // prow[RI]: the pivot's reciprocal
     const int lane = g.lane;
     const bool hi_half = (threadIdx.x & 32) != 0;
@@ -442,6 +449,31 @@ struct Smp {
         }
       }
     }
+    // carried proposal of the next iteration (see amm): formed here, where the factor rows are
+    // still in registers; skipped when the next proposal would need an older factor
+    if (NB != nullptr && (rank == d || m <= 2 * d)) {
+      const mmb_rng rn1 = mmb_rng_make(A.seed, chain, (uint32_t)(it + 1), (uint32_t)b, MMB_SUB_NORMAL);
+      double z1n = 0.0, z2n = 0.0;
+      if (inb) mmb_normal_pair(&rn1, (uint32_t)lane, &z1n, &z2n);
+      double a = 0.0;
+      if (inb) a = fma(NB->sigl[lane * d + lane], z1n, a);
+      if (m > 2 * d) {
+        prow[lane] = z2n;
+        grp_sync();
+        // rows are zero past the lane's own step, so the full sweep adds exact zeros
+        double y = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; k += 2) {
+          const double2 zz = *(const double2*)(prow + k);
+          y = fma(Lrow[k], zz.x, y);
+          if (k + 1 < DMAX) y = fma(Lrow[k + 1], zz.y, y);
+        }
+        grp_sync();
+        a = NB->beta * a + (1.0 - NB->beta) * y;
+      }
+      if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
+      if (lane == 0) NB->t_xtag[c] = xtag(A, it + 1);
+    }
     if (rank == d && inb) {  // write the factor back in slot form
       bool before = true;
 #pragma unroll
@@ -471,7 +503,21 @@ struct Smp {
 
   // ---------------------------------------------------------------- AMM
   // amm.jl:66-108.  LDS per chain: mat[TP] | z2[DP] | vv[DP] | mv[DP] | ia[2*DP ints]
-  __device__ __forceinline__ static void amm(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,
+  // Carried proposal (32-lane groups, diagonal SigmaL): the proposal of the NEXT iteration,
+  // x' - v = SigmaL z1' [beta * . + (1 - beta) SigmaLm z2'] (amm.jl:72-76), depends only on
+  // that iteration's draws (Philox keyed by the iteration), the tune m after this update and
+  // the factor this update computes -- and v is unchanged in between (only this block samples
+  // its nodes).  So it is formed right after the factorization, with the factor rows still in
+  // registers (no pivot decode), and carried through HBM (t_xnext, 30 doubles) instead of
+  // re-reading the factor (465 doubles) next time.  Same operations in the same order, so the
+  // draws are bit-identical; the tag (host epoch, iteration) makes any host write of the chain
+  // state or a skipped update fall back to the direct path.
+  static constexpr bool CARRY = (G == 32 && R == 1);
+  __device__ __forceinline__ static int64_t xtag(const SweepArgs& A, int64_t it) {
+    return (A.xepoch << 32) | (int64_t)(uint32_t)it;
+  }
+  __device__ __forceinline__ static void amm(const SweepArgs& A, const DBlock& B, int c, uint32_t chain,
+                             int64_t it, int b, const mmb_rng& rn,
                              const mmb_rng& ru, bool adapt, St& s, const Lc& l, const Grp<G>& g,
                              double* lds, double upre) {
     const int d = B.d;
@@ -492,6 +538,8 @@ struct Smp {
       mv[r] = e < d ? B.t_Mv[(size_t)c * DP + e] : 0.0;
     }
     const bool fresh = adapt && !(fl & 1);
+    bool carried = false;
+    if constexpr (CARRY) carried = B.t_xtag != nullptr && !fresh && B.t_xtag[c] == xtag(A, it);
     if (fresh) {  // setadapt!: m = 0, Mv = v (aliased), Mvv = v v', SigmaLm = 0
       m = 0;
       fl = (fl | 2) & ~4;
@@ -501,6 +549,9 @@ struct Smp {
     fl = adapt ? (fl | 1) : (fl & ~1);
     MMB_PROF_MARK(1, g.lane)
     // proposal: x = SigmaL * z1 [; x = beta*x + (1-beta)*SigmaLm*z2]; x += v
+    if (carried) {
+      x[0] = g.lane < d ? B.t_xnext[(size_t)c * DP + g.lane] : 0.0;
+    } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       int e = r * G + g.lane;
@@ -576,6 +627,7 @@ struct Smp {
 #pragma unroll
       for (int r = 0; r < R; ++r) x[r] = B.beta * x[r] + (1.0 - B.beta) * y[r];
     }
+    }  // !carried
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = x[r] + v[r];
     MMB_PROF_MARK(2, g.lane)
@@ -663,8 +715,10 @@ struct Smp {
       int rank = d;  // timing experiment only
 #else
       int rank;
+      const bool carry = CARRY && B.t_xtag != nullptr && B.sigl_diag;
 #ifndef MMB_PCHOL_GENERIC
-      if constexpr (G == 32 && R == 1) rank = pchol32(d, mat, (double*)ia, pks, g);
+      if constexpr (G == 32 && R == 1)
+        rank = pchol32(d, mat, (double*)ia, pks, g, carry ? &B : nullptr, A, c, chain, it, b, m);
       else
 #endif
         rank = pchol(d, mat, (double*)ia, pks, g);

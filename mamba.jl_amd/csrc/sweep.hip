@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
           if constexpr ((KINDS >> MMB_SAMPLER_AMWG) & 1u) S::amwg(A, B, c, rn, ru, adapt, s, l, g);
           break;
         case MMB_SAMPLER_AMM:
-          if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) S::amm(A, B, c, rn, ru, adapt, s, l, g, lds,
+          if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) S::amm(A, B, c, chain, it, b, rn, ru, adapt, s, l, g, lds,
                                                                         G == 32 ? S::lane_value(pre, b) : 0.0);
           break;
         case MMB_SAMPLER_SLICE:
