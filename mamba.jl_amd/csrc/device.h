@@ -184,6 +184,10 @@ struct Grp {
       x += other_d<4>(x);
       return x;
     }
+    if (G == 16) {  // one DPP row: four stages, no permlane
+      x += other_d<0>(x); x += other_d<1>(x); x += other_d<2>(x); x += other_d<3>(x);
+      return x;
+    }
 #pragma unroll
     for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
     return x;
@@ -195,6 +199,13 @@ struct Grp {
       x += other_d<2>(x); y += other_d<2>(y);
       x += other_d<3>(x); y += other_d<3>(y);
       x += other_d<4>(x); y += other_d<4>(y);
+      return;
+    }
+    if (G == 16) {
+      x += other_d<0>(x); y += other_d<0>(y);
+      x += other_d<1>(x); y += other_d<1>(y);
+      x += other_d<2>(x); y += other_d<2>(y);
+      x += other_d<3>(x); y += other_d<3>(y);
       return;
     }
 #pragma unroll

@@ -1068,6 +1068,31 @@ int mmb_get_draws(mmb_engine* e, double* draws) {
 
 // ---------------------------------------------------------------- tune (canonical layout)
 
+// The 32-lane factorization (samplers.h pchol32: rats, node IR) keeps the AMM factor in
+// POSITION form on device -- row at pivot position t at tri(t) + k, k = 0..t, plus one byte per
+// element holding its position -- while the canonical tune layout (and the oracle) use the slot
+// form L[e][step k] -> slot(e, piv[k]), diagonal at slot(e, e), plus the pivot order.
+static bool amm_posform(const mmb_engine* e) { return e->model == MMB_MODEL_RATS || e->model == MMB_MODEL_IR; }
+static int tri_(int i) { return i * (i + 1) / 2; }
+static int slot_(int i, int k) { return i >= k ? tri_(i) + k : tri_(k) + i; }
+// position form (lp, pos) -> slot form (ls, piv); one chain, d x d
+static void pos_to_slot(int d, const double* lp, const uint8_t* pos, double* ls, uint8_t* piv) {
+  for (int e = 0; e < d; ++e) piv[pos[e] < d ? pos[e] : e] = (uint8_t)e;
+  for (int e = 0; e < d; ++e) {
+    const int pe = pos[e] < d ? pos[e] : e;
+    for (int k = 0; k < pe; ++k) ls[slot_(e, piv[k])] = lp[tri_(pe) + k];
+    ls[slot_(e, e)] = lp[tri_(pe) + pe];
+  }
+}
+static void slot_to_pos(int d, const double* ls, const uint8_t* piv, double* lp, uint8_t* pos) {
+  for (int k = 0; k < d; ++k) pos[piv[k] < d ? piv[k] : k] = (uint8_t)k;
+  for (int e = 0; e < d; ++e) {
+    const int pe = pos[e];
+    for (int k = 0; k < pe; ++k) lp[tri_(pe) + k] = ls[slot_(e, piv[k])];
+    lp[tri_(pe) + pe] = ls[slot_(e, e)];
+  }
+}
+
 int mmb_get_tune(mmb_engine* e, double* tune) {
   if (!e || !tune) return fail(e, MMB_E_ARG, "null argument");
   if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
@@ -1106,9 +1131,17 @@ int mmb_get_tune(mmb_engine* e, double* tune) {
         p += h.d;
         for (int s = 0; s < h.T; ++s) p[s] = mvv[k * TP + s];
         p += h.T;
-        for (int s = 0; s < h.T; ++s) p[s] = ls[k * TP + s];
-        p += h.T;
-        for (int i = 0; i < h.d; ++i) p[i] = pv[k * DP + i];
+        if (amm_posform(e)) {
+          std::vector<uint8_t> piv(h.d);
+          std::fill(p, p + h.T, 0.0);
+          pos_to_slot(h.d, &ls[k * TP], &pv[k * DP], p, piv.data());
+          p += h.T;
+          for (int i = 0; i < h.d; ++i) p[i] = piv[i];
+        } else {
+          for (int s = 0; s < h.T; ++s) p[s] = ls[k * TP + s];
+          p += h.T;
+          for (int i = 0; i < h.d; ++i) p[i] = pv[k * DP + i];
+        }
       }
     } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
       std::vector<double> nt;
@@ -1164,9 +1197,15 @@ int mmb_set_tune(mmb_engine* e, const double* tune) {
         p += h.d;
         for (int s = 0; s < h.T; ++s) mvv[k * TP + s] = p[s];
         p += h.T;
-        for (int s = 0; s < h.T; ++s) ls[k * TP + s] = p[s];
-        p += h.T;
-        for (int i = 0; i < h.d; ++i) pv[k * DP + i] = (uint8_t)p[i];
+        if (amm_posform(e)) {
+          std::vector<uint8_t> piv(h.d);
+          for (int i = 0; i < h.d; ++i) piv[i] = (uint8_t)p[h.T + i];
+          slot_to_pos(h.d, p, piv.data(), &ls[k * TP], &pv[k * DP]);
+        } else {
+          for (int s = 0; s < h.T; ++s) ls[k * TP + s] = p[s];
+          p += h.T;
+          for (int i = 0; i < h.d; ++i) pv[k * DP + i] = (uint8_t)p[i];
+        }
       }
       if ((rc = h2d(e, h.Mv, mv)) || (rc = h2d(e, h.Mvv, mvv)) || (rc = h2d(e, h.Ls, ls)) ||
           (rc = h2d(e, h.piv, pv)))

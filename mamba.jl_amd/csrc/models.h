@@ -14,26 +14,31 @@ struct Mdl;
 // ------------------------------------------------------------------ rats
 // doc/examples/rats.jl:48-97.  Device value layout per chain (72 doubles):
 //   [0,32) alpha (30 + pad) | [32,64) beta | 64 s2_c | 65 mu_alpha | 66 s2_alpha |
-//   67 mu_beta | 68 s2_beta.   Group = 32 lanes, lane i <-> rat i.
+//   67 mu_beta | 68 s2_beta.
+// Group = 32 lanes, two chains per wave: rat e <-> lane e (register slot R = 1; the model code
+// is written for R rats per lane).  A 16-lane, two-rats-per-lane layout (four chains per wave,
+// half the instructions per chain in each pivoted-Cholesky step) was measured at 0.318 vs
+// 0.220 ms per sweep: LDS caps both layouts at 32 chains per CU and the factorization is
+// latency-bound, so 4 waves of 2 chains beat 2 waves of 4.
 template <>
 struct Mdl<MMB_MODEL_RATS> {
   static constexpr int G = 32, R = 1, DMAX = 30, DP = 32, TP = 480, VS = 72, PMON = 3;
   static constexpr int LDS_DBL = TP + 4 * DP;  // matrix + 4 vectors (the stash reuses idle ones)
-  struct St { double a, b, s2c, mua, s2a, mub, s2b; };
-  struct Lc { const double* y; };  // this lane's 5 observations (global, L1-resident)
+  struct St { double a[R], b[R]; double s2c, mua, s2a, mub, s2b; };
+  struct Lc { int dummy; };
+  __device__ __forceinline__ static int elem(int r, int lane) { return r * G + lane; }
 
   __host__ __device__ static int lds_stride(const SweepArgs&) { return LDS_DBL; }
-  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc& l, double*) {
+  __device__ __forceinline__ static void load(const SweepArgs& A, int c, int lane, St& s, Lc&, double*) {
     const double* v = A.vals + (size_t)c * VS;
-    s.a = v[lane];
-    s.b = v[32 + lane];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { s.a[r] = v[elem(r, lane)]; s.b[r] = v[32 + elem(r, lane)]; }
     s.s2c = v[64]; s.mua = v[65]; s.s2a = v[66]; s.mub = v[67]; s.s2b = v[68];
-    l.y = A.data0 + (lane < 30 ? lane : 0) * 5;
   }
   __device__ __forceinline__ static void store(const SweepArgs& A, int c, int lane, const St& s) {
     double* v = A.vals + (size_t)c * VS;
-    v[lane] = s.a;
-    v[32 + lane] = s.b;
+#pragma unroll
+    for (int r = 0; r < R; ++r) { v[elem(r, lane)] = s.a[r]; v[32 + elem(r, lane)] = s.b[r]; }
     if (lane == 0) { v[64] = s.s2c; v[65] = s.mua; v[66] = s.s2a; v[67] = s.mub; v[68] = s.s2b; }
   }
   __device__ __forceinline__ static void monitored(const SweepArgs& A, const St& s, double* out) {
@@ -59,14 +64,14 @@ struct Mdl<MMB_MODEL_RATS> {
   // ia): alpha -> vvs, beta -> mvs, scalars -> the tail of z2s (pivot indices use 30 ints)
   __device__ __forceinline__ static void stash(double* lds, const St& s, int lane) {
     double* q = lds + TP;
-    q[DP + lane] = s.a;
-    q[2 * DP + lane] = s.b;
+#pragma unroll
+    for (int r = 0; r < R; ++r) { q[DP + elem(r, lane)] = s.a[r]; q[2 * DP + elem(r, lane)] = s.b[r]; }
     if (lane == 0) { q[16] = s.s2c; q[17] = s.mua; q[18] = s.s2a; q[19] = s.mub; q[20] = s.s2b; }
   }
   __device__ __forceinline__ static void unstash(const double* lds, St& s, int lane) {
     const double* q = lds + TP;
-    s.a = q[DP + lane];
-    s.b = q[2 * DP + lane];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { s.a[r] = q[DP + elem(r, lane)]; s.b[r] = q[2 * DP + elem(r, lane)]; }
     s.s2c = q[16]; s.mua = q[17]; s.s2a = q[18]; s.mub = q[19]; s.s2b = q[20];
   }
   // select chains (a switch here is turned into a dynamically indexed private array)
@@ -101,17 +106,26 @@ struct Mdl<MMB_MODEL_RATS> {
   // unlist(block, transform) into lane-owned element slots
   __device__ __forceinline__ static void unlist(const DBlock& B, const St& s, int lane, double* x) {
     if (is_vec(B.nodes[0])) {
-      x[0] = lane < 30 ? (B.nodes[0] == MMB_RATS_ALPHA ? s.a : s.b) : 0.0;
+      const bool al = B.nodes[0] == MMB_RATS_ALPHA;
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = elem(r, lane) < 30 ? (al ? s.a[r] : s.b[r]) : 0.0;
     } else {
       int n = lane_node(B, lane);
       double v = scalar(s, n);
       x[0] = lane < B.d ? ((B.transform && positive(n)) ? mmb_log(v) : v) : 0.0;
+#pragma unroll
+      for (int r = 1; r < R; ++r) x[r] = 0.0;
     }
   }
   __device__ __forceinline__ static void relist(const DBlock& B, St& s, const Grp<G>& g, const double* x) {
     if (is_vec(B.nodes[0])) {
-      if (B.nodes[0] == MMB_RATS_ALPHA) s.a = g.lane < 30 ? x[0] : s.a;
-      else s.b = g.lane < 30 ? x[0] : s.b;
+      const bool al = B.nodes[0] == MMB_RATS_ALPHA;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool in = elem(r, g.lane) < 30;
+        if (al) s.a[r] = in ? x[r] : s.a[r];
+        else s.b[r] = in ? x[r] : s.b[r];
+      }
     } else {
       for (int e = 0; e < B.d; ++e) {
         double v = g.bcast(x[0], e);
@@ -120,19 +134,31 @@ struct Mdl<MMB_MODEL_RATS> {
       }
     }
   }
-  // lane partial of sum_t (y - (alpha + beta*Xm))^2 for this lane's rat
-  __device__ __forceinline__ static double ssr_lane(const SweepArgs& A, const Lc& l, double a, double b, int lane) {
+  // lane partial of sum_t (y - (alpha + beta*Xm))^2 over this lane's rats (slot order)
+  __device__ __forceinline__ static double ssr_lane(const SweepArgs& A, const Lc&, const double* a, const double* b,
+                                                    int lane) {
     double acc = 0.0;
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      double mu = a + b * A.xm[t];
-      double r = l.y[t] - mu;
-      acc = fma(r, r, acc);
+    for (int r = 0; r < R; ++r) {
+      const int e = elem(r, lane);
+      const double* y = A.data0 + (e < 30 ? e : 0) * 5;
+      double part = 0.0;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        double mu = a[r] + b[r] * A.xm[t];
+        double rr = y[t] - mu;
+        part = fma(rr, rr, part);
+      }
+      acc += e < 30 ? part : 0.0;
     }
-    return lane < 30 ? acc : 0.0;
+    return acc;
   }
-  __device__ __forceinline__ static double normsum_lane(double mu, double sig, double logsig, double x, int lane) {
-    return lane < 30 ? d_normlogpdf(mu, sig, logsig, x) : 0.0;
+  __device__ __forceinline__ static double normsum_lane(double mu, double sig, double logsig, const double* x,
+                                                        int lane) {
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc += elem(r, lane) < 30 ? d_normlogpdf(mu, sig, logsig, x[r]) : 0.0;
+    return acc;
   }
   // Invariants of a vector block's logpdf! that do not depend on the block vector:
   // prior sd / log sd of the block node and y's ScalMat constants.  Computed once per
@@ -153,10 +179,9 @@ struct Mdl<MMB_MODEL_RATS> {
   // logpdf!([alpha] or [beta], x): prior (params \ targets) then y (d_iso expanded)
   __device__ __forceinline__ static double logf_vec(const SweepArgs& A, const VecCtx& c,
                                                     const St& s, const Lc& l, const Grp<G>& g,
-                                                    double x) {
-    const double a = c.al ? x : s.a, b = c.al ? s.b : x;
+                                                    const double* x) {
     double pr = normsum_lane(c.mu, c.sig, c.logsig, x, g.lane);
-    double ss = ssr_lane(A, l, a, b, g.lane);
+    double ss = c.al ? ssr_lane(A, l, x, s.b, g.lane) : ssr_lane(A, l, s.a, x, g.lane);
     g.sum2(pr, ss);
     double lp = 0.0 + pr;
     if (!isfinite(lp)) return lp;
@@ -168,7 +193,7 @@ struct Mdl<MMB_MODEL_RATS> {
   __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep& c,
                                                   const St& s, const Lc& l, const Grp<G>& g,
                                                   const double* x) {
-    if (is_vec(B.nodes[0])) return logf_vec(A, c, s, l, g, x[0]);
+    if (is_vec(B.nodes[0])) return logf_vec(A, c, s, l, g, x);
     return logf(A, B, s, l, g, x);
   }
   // logpdf!(block, x)
@@ -176,8 +201,7 @@ struct Mdl<MMB_MODEL_RATS> {
                                 const Grp<G>& g, const double* x) {
     St s = s0;
     relist(B, s, g, x);
-    const double NEG = -__builtin_inf();
-    if (is_vec(B.nodes[0])) return logf_vec(A, vec_ctx(B, s0), s0, l, g, x[0]);
+    if (is_vec(B.nodes[0])) return logf_vec(A, vec_ctx(B, s0), s0, l, g, x);
     // scalar block: params (none is a target of another) in block order
     unsigned tm = 0;
     double lp = 0.0;
@@ -210,7 +234,6 @@ struct Mdl<MMB_MODEL_RATS> {
       lp += d_iso(150, sqrt(s.s2c), ss);
     }
     return lp;
-    (void)NEG;
   }
   // The random draw of a conjugate block does not depend on the chain state: a Gamma(a)
   // variate for the s2 blocks (rand(InverseGamma(a, b)) = b / G, shape a fixed by the
@@ -234,7 +257,10 @@ struct Mdl<MMB_MODEL_RATS> {
       s.s2c = b / draw;
     } else if (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_MU_BETA) {
       const bool al = n == MMB_RATS_MU_ALPHA;
-      double sum = g.sum(g.lane < 30 ? blend(al, s.a, s.b) : 0.0);
+      double part = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) part += elem(r, g.lane) < 30 ? blend(al, s.a[r], s.b[r]) : 0.0;
+      double sum = g.sum(part);
       double s2 = blend(al, s.s2a, s.s2b);
       double var0 = 1000.0 * 1000.0;
       double vv = 1.0 / (30.0 / s2 + 1.0 / var0);
@@ -245,8 +271,13 @@ struct Mdl<MMB_MODEL_RATS> {
     } else {
       const bool al = n == MMB_RATS_S2_ALPHA;
       double mu = blend(al, s.mua, s.mub);
-      double r = blend(al, s.a, s.b) - mu;
-      double ss = g.sum(g.lane < 30 ? r * r : 0.0);
+      double part = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double rr = blend(al, s.a[r], s.b[r]) - mu;
+        part += elem(r, g.lane) < 30 ? rr * rr : 0.0;
+      }
+      double ss = g.sum(part);
       double v = (ss / 2.0 + 0.001) / draw;
       s.s2a = blend(al, v, s.s2a);
       s.s2b = blend(al, s.s2b, v);

@@ -373,10 +373,15 @@ struct Smp {
   // iteration (z2' = the second normal of each element's pair from rn1), formed from the
   // factor rows still in registers: P L z2' (amm.jl:74), row e = sum_k L[pos e][k] z2'[k],
   // k ascending -- the order of the direct matvec in amm().
+  //
+  // On full rank the factor is left in `mat` in POSITION form (row at pivot position t, i.e.
+  // row piv[t] of P'L... stored at tri(t) .. tri(t) + t, step order), and *pos receives this
+  // lane's position; amm() stores it with the position bytes (the host converts to the
+  // canonical slot form + pivot order, engine.cpp).
   __device__ __forceinline__ static int pchol32(int d, double* mat, double* prow, int* pks, const Grp<G>& g,
-                                                const DBlock* NB = nullptr, const SweepArgs& A = SweepArgs{},
-                                                int c = 0, uint32_t chain = 0, int64_t it = 0, int b = 0,
-                                                int m = 0) {
+                                                int* pos_out, const DBlock* NB = nullptr,
+                                                const SweepArgs& A = SweepArgs{}, int c = 0, uint32_t chain = 0,
+                                                int64_t it = 0, int b = 0, int m = 0) {
     constexpr int RI = DMAX;  // prow[RI]: the pivot's reciprocal
     const int lane = g.lane;
     const bool hi_half = (threadIdx.x & 32) != 0;
@@ -388,26 +393,34 @@ struct Smp {
     for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
     bool done = !inb;
     int rank = d;
+    int pe = 0;  // this lane's pivot position
     bool live = true;
 #pragma unroll
     for (int j = 0; j < DMAX; ++j) {
       if (live && j < d) {
+        MMB_PROF_START
         const double dl = diag0 - work;
+        // every lane forms sqrt / reciprocal of its own candidate before the search ends
+        // (independent of it, so its latency overlaps the reductions); the pivot lane's pair
+        // is the one used (out of the fast range: sqrt() and division on the pivot lane)
+        const double ajj_s = mmb_sqrt_inrange(dl);
+        const double rinv_s = mmb_rcp_inrange(ajj_s);
         // key: high word of a positive candidate, INT_MAX for a NaN candidate, else -1
         // (three independent selects: no branchy nest for the compiler to serialise)
         const int hiw = (int)(mmb_d2u(dl) >> 32);
         int key = dl > 0.0 ? hiw : -1;
         key = isnan(dl) ? 0x7fffffff : key;
         key = done ? -1 : key;
-        const int m = gmax_i32(key);
-        const uint32_t win = (uint32_t)(__ballot(key == m) >> (threadIdx.x & 32));
+        const int mx = gmax_i32(key);
+        const uint32_t win = (uint32_t)(__ballot(key == mx) >> (threadIdx.x & 32));
         int p = __builtin_ctz(win | 0x80000000u);
-        bool pos = m >= 0;
-        if (!(m < 0 || (m != 0x7fffffff && __builtin_popcount(win) == 1))) {
+        bool pos = mx >= 0;
+        if (!(mx < 0 || (mx != 0x7fffffff && __builtin_popcount(win) == 1))) {
           double val;
           p = pivot_exact(dl, done, pks, j, d, (int*)prow, &val);
           pos = val > 0.0;
         }
+        MMB_PROF_MARK(10, lane)
         if (!pos) {
           rank = j;
           live = false;
@@ -419,18 +432,17 @@ struct Smp {
 #pragma unroll
             for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
             if (j & 1) prow[j - 1] = Lrow[j - 1];
-            double rinv;
-            if (mmb_fast_range(dl)) {  // the pivot's sqrt and reciprocal, IEEE results (device.h)
-              ajj = mmb_sqrt_inrange(dl);
-              rinv = mmb_rcp_inrange(ajj);
-            } else {
+            ajj = ajj_s;  // IEEE results in the fast range (device.h)
+            double rinv = rinv_s;
+            if (!mmb_fast_range(dl)) {
               ajj = sqrt(dl);
               rinv = 1.0 / ajj;
             }
             prow[RI] = rinv;
           }
           grp_sync();
-          if (piv) Lrow[j] = ajj;
+          MMB_PROF_MARK(11, lane)
+          if (piv) { Lrow[j] = ajj; pe = j; }
           done = done || piv;
           if (!done) {
             double t0 = 0.0, t1 = 0.0;
@@ -446,6 +458,7 @@ struct Smp {
             work = work + lij * lij;
           }
           grp_sync();
+          MMB_PROF_MARK(12, lane)
         }
       }
     }
@@ -474,21 +487,17 @@ struct Smp {
       if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
       if (lane == 0) NB->t_xtag[c] = xtag(A, it + 1);
     }
-    if (rank == d && inb) {  // write the factor back in slot form
-      bool before = true;
+    if (rank == d && inb) {  // the factor in position form: row at position pe at tri(pe) + k
+      // one store per k from every lane, no exec-mask change: entries past the row's end
+      // (k > pe, exact zeros) go to the lane's own dummy slot in the idle pivot-row buffer
+      const int base = mmb_tri(pe);
 #pragma unroll
       for (int k = 0; k < DMAX; ++k) {
-        if (k < d) {
-          const int q = pks[k];
-          if (q == lane) {
-            mat[mmb_tri(lane) + lane] = Lrow[k];
-            before = false;
-          } else if (before) {
-            mat[mmb_slot(lane, q)] = Lrow[k];
-          }
-        }
+        double* dst = k <= pe ? mat + base + k : prow + lane;
+        *dst = Lrow[k];
       }
     }
+    *pos_out = pe;
     return rank;
   }
 
@@ -513,6 +522,9 @@ struct Smp {
   // draws are bit-identical; the tag (host epoch, iteration) makes any host write of the chain
   // state or a skipped update fall back to the direct path.
   static constexpr bool CARRY = (G == 32 && R == 1);
+  // factor storage on device: position form + position bytes (pchol32) or slot form + pivot
+  // order (pchol); the host converts to the canonical slot form (engine.cpp mmb_get_tune)
+  static constexpr bool POSFORM = (G == 32 && R == 1);
   __device__ __forceinline__ static int64_t xtag(const SweepArgs& A, int64_t it) {
     return (A.xepoch << 32) | (int64_t)(uint32_t)it;
   }
@@ -550,7 +562,11 @@ struct Smp {
     MMB_PROF_MARK(1, g.lane)
     // proposal: x = SigmaL * z1 [; x = beta*x + (1-beta)*SigmaLm*z2]; x += v
     if (carried) {
-      x[0] = g.lane < d ? B.t_xnext[(size_t)c * DP + g.lane] : 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = r * G + g.lane;
+        x[r] = e < d ? B.t_xnext[(size_t)c * DP + e] : 0.0;
+      }
     } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -592,6 +608,20 @@ struct Smp {
 #pragma unroll
         for (int u = 0; u < NT; ++u)
           if (u * G + g.lane < T) mat[u * G + g.lane] = lt[u];
+        if constexpr (POSFORM) {
+          // position form: this lane's row starts at tri(pos e); y = sum_{k <= pos e} L z2s[k]
+          // in k order (the diagonal last), as the slot-form matvec below
+          const int e = g.lane;
+          const int pe = e < d ? (int)B.t_piv[(size_t)c * DP + e] : 0;
+          if (e < d) z2s[e] = z2[0];
+          grp_sync();
+          const double* row = mat + mmb_tri(pe);
+          double a = 0.0;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k)
+            if (k < d) a = k <= pe ? fma(row[k], z2s[k], a) : a;
+          if (e < d) y[0] = a;
+        } else {
         // pivot order: the chain's DP bytes as DP/4 words in registers (uniform per group),
         // so the matvec's LDS reads are independent of each other (no ia[k] -> mat chain)
         uint32_t pw[DP / 4];
@@ -623,6 +653,7 @@ struct Smp {
           }
           if (e < d) y[r] = fma(mat[mmb_tri(e) + e], z2s[pe], a);
         }
+        }  // !POSFORM
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) x[r] = B.beta * x[r] + (1.0 - B.beta) * y[r];
@@ -717,8 +748,9 @@ struct Smp {
       int rank;
       const bool carry = CARRY && B.t_xtag != nullptr && B.sigl_diag;
 #ifndef MMB_PCHOL_GENERIC
+      int pe = 0;
       if constexpr (G == 32 && R == 1)
-        rank = pchol32(d, mat, (double*)ia, pks, g, carry ? &B : nullptr, A, c, chain, it, b, m);
+        rank = pchol32(d, mat, (double*)ia, pks, g, &pe, carry ? &B : nullptr, A, c, chain, it, b, m);
       else
 #endif
         rank = pchol(d, mat, (double*)ia, pks, g);
@@ -731,7 +763,11 @@ struct Smp {
         for (int u = 0; u < NT; ++u)
           if (u * G + g.lane < T) Ls[u * G + g.lane] = mat[u * G + g.lane];
         uint8_t* pv = B.t_piv + (size_t)c * DP;
-        for (int k = g.lane; k < d; k += G) pv[k] = (uint8_t)pks[k];
+        if constexpr (POSFORM) {
+          if (g.lane < d) pv[g.lane] = (uint8_t)pe;  // position of element lane
+        } else {
+          for (int k = g.lane; k < d; k += G) pv[k] = (uint8_t)pks[k];
+        }
         if (g.lane == 0) B.t_flags[c] = fl | 4;
       }
       M::unstash(lds, s, g.lane);

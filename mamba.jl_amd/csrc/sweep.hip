@@ -17,8 +17,9 @@ void mmb_prof_dump() {
   unsigned long long h[32];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mmb_prof), sizeof h) != hipSuccess) return;
   const char* names[] = {"-", "amm:load m/fl/Mv", "amm:proposal", "amm:logf x2+accept", "amm:moments+Sigma",
-                         "amm:pchol", "amm:store", "gibbs", "iteration", "count"};
-  for (int i = 1; i < 10; ++i) fprintf(stderr, "MMB_PROF %-22s %llu\n", names[i], h[i]);
+                         "amm:pchol", "amm:store", "gibbs", "iteration", "count", "pchol:search",
+                         "pchol:pivot row", "pchol:dot", "pchol:tail"};
+  for (int i = 1; i < 14; ++i) fprintf(stderr, "MMB_PROF %-22s %llu\n", names[i], h[i]);
 }
 #endif
 
