@@ -684,35 +684,31 @@ struct Smp {
         for (int r = 0; r < R; ++r) mv[r] = p * mv[r] + q * v[r];
       }
       grp_sync();
+      // (v[e], Mv[e]) pairs interleaved over the vvs|mvs scratch: one 16-byte read per index
+      double2* vm = (double2*)vvs;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         int e = r * G + g.lane;
-        if (e < d) { vvs[e] = v[r]; mvs[e] = mv[r]; }
+        if (e < d) vm[e] = make_double2(v[r], mv[r]);
       }
-      grp_sync();
       const double cc = (B.scale * B.scale / (double)d) / p;
       double* Mvv = B.t_Mvv + (size_t)c * TP;
       // fresh: Mvv = v_old v_old' was formed before the proposal; v_old is still unlist()
       // of the state `s`, so recompute it from s here (same products).
       double vold[R];
-      if (fresh) M::unlist(B, s, g.lane, vold);
       if (fresh) {
-        grp_sync();
+        M::unlist(B, s, g.lane, vold);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           int e = r * G + g.lane;
           if (e < d) z2s[e] = vold[r];
         }
-        grp_sync();
       }
-      if (!fresh) {  // stage Mvv in LDS: all loads in flight at once (one HBM latency)
-        double lt[NT];
+      grp_sync();
+      // the lane's own Mvv slots straight into registers, all loads in flight at once
+      double lt[NT];
 #pragma unroll
-        for (int u = 0; u < NT; ++u) lt[u] = (u * G + g.lane < T) ? Mvv[u * G + g.lane] : 0.0;
-#pragma unroll
-        for (int u = 0; u < NT; ++u)
-          if (u * G + g.lane < T) mat[u * G + g.lane] = lt[u];
-      }
+      for (int u = 0; u < NT; ++u) lt[u] = (!fresh && u * G + g.lane < T) ? Mvv[u * G + g.lane] : 0.0;
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         int t = u * G + g.lane;
@@ -722,10 +718,11 @@ struct Smp {
         if (t < T) {
           int i, k;
           slot_ik(t, i, k);
-          double old = fresh ? z2s[i] * z2s[k] : mat[t];
-          double nv = p * old + (q * vvs[k]) * vvs[i];
+          const double2 a = vm[k], bi = vm[i];
+          double old = fresh ? z2s[i] * z2s[k] : lt[u];
+          double nv = p * old + (q * a.x) * bi.x;
           Mvv[t] = nv;
-          mat[t] = cc * (nv - mvs[k] * mvs[i]);
+          mat[t] = cc * (nv - a.y * bi.y);
         }
       }
       grp_sync();
