@@ -391,6 +391,7 @@ struct Smp {
     double Lrow[DMAX];
 #pragma unroll
     for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
+    MMB_PROF_START
     bool done = !inb;
     int rank = d;
     int pe = 0;  // this lane's pivot position
@@ -398,7 +399,6 @@ struct Smp {
 #pragma unroll
     for (int j = 0; j < DMAX; ++j) {
       if (live && j < d) {
-        MMB_PROF_START
         const double dl = diag0 - work;
         // every lane forms sqrt / reciprocal of its own candidate before the search ends
         // (independent of it, so its latency overlaps the reductions); the pivot lane's pair
@@ -420,7 +420,6 @@ struct Smp {
           p = pivot_exact(dl, done, pks, j, d, (int*)prow, &val);
           pos = val > 0.0;
         }
-        MMB_PROF_MARK(10, lane)
         if (!pos) {
           rank = j;
           live = false;
@@ -441,7 +440,6 @@ struct Smp {
             prow[RI] = rinv;
           }
           grp_sync();
-          MMB_PROF_MARK(11, lane)
           if (piv) { Lrow[j] = ajj; pe = j; }
           done = done || piv;
           if (!done) {
@@ -458,10 +456,10 @@ struct Smp {
             work = work + lij * lij;
           }
           grp_sync();
-          MMB_PROF_MARK(12, lane)
         }
       }
     }
+    MMB_PROF_MARK(10, lane)
     // carried proposal of the next iteration (see amm): formed here, where the factor rows are
     // still in registers; skipped when the next proposal would need an older factor
     if (NB != nullptr && (rank == d || m <= 2 * d)) {
@@ -487,6 +485,7 @@ struct Smp {
       if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
       if (lane == 0) NB->t_xtag[c] = xtag(A, it + 1);
     }
+    MMB_PROF_MARK(11, lane)
     if (rank == d && inb) {  // the factor in position form: row at position pe at tri(pe) + k
       // one store per k from every lane, no exec-mask change: entries past the row's end
       // (k > pe, exact zeros) go to the lane's own dummy slot in the idle pivot-row buffer
@@ -497,10 +496,27 @@ struct Smp {
         *dst = Lrow[k];
       }
     }
+    MMB_PROF_MARK(12, lane)
     *pos_out = pe;
     return rank;
   }
 
+  // (i, k) of every packed slot, i << 8 | k, one table per workgroup in LDS (filled once per
+  // launch by ik_fill): the moment update reads it instead of inverting tri() per slot
+  static constexpr bool IKTAB = (G == 32);
+  __device__ __forceinline__ static uint16_t* ik_table() {
+    __shared__ uint16_t tab[IKTAB ? TP : 1];
+    return tab;
+  }
+  __device__ __forceinline__ static void ik_fill() {
+    if constexpr (IKTAB) {
+      for (int t = (int)threadIdx.x; t < TP; t += (int)blockDim.x) {
+        int i, k;
+        slot_ik(t, i, k);
+        ik_table()[t] = (uint16_t)(i << 8 | k);
+      }
+    }
+  }
   // (i, k) of packed slot s = tri(i) + k: float square root estimate, integer correction
   __device__ __forceinline__ static void slot_ik(int s, int& i, int& k) {
     int ii = (int)((sqrtf((float)(8 * s + 1)) - 1.0f) * 0.5f);
@@ -717,7 +733,13 @@ struct Smp {
         asm volatile("" : "+v"(t));
         if (t < T) {
           int i, k;
-          slot_ik(t, i, k);
+          if constexpr (IKTAB) {
+            const int w = ik_table()[t];
+            i = w >> 8;
+            k = w & 255;
+          } else {
+            slot_ik(t, i, k);
+          }
           const double2 a = vm[k], bi = vm[i];
           double old = fresh ? z2s[i] * z2s[k] : lt[u];
           double nv = p * old + (q * a.x) * bi.x;

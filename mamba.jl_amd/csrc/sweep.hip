@@ -17,8 +17,8 @@ void mmb_prof_dump() {
   unsigned long long h[32];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mmb_prof), sizeof h) != hipSuccess) return;
   const char* names[] = {"-", "amm:load m/fl/Mv", "amm:proposal", "amm:logf x2+accept", "amm:moments+Sigma",
-                         "amm:pchol", "amm:store", "gibbs", "iteration", "count", "pchol:search",
-                         "pchol:pivot row", "pchol:dot", "pchol:tail"};
+                         "amm:pchol", "amm:store", "gibbs", "iteration", "count", "pchol:steps",
+                         "pchol:carry", "pchol:writeback", "-"};
   for (int i = 1; i < 14; ++i) fprintf(stderr, "MMB_PROF %-22s %llu\n", names[i], h[i]);
 }
 #endif
@@ -45,6 +45,10 @@ __global__ __launch_bounds__(256, sweep_waves<MODEL>()) void sweep_kernel(const 
   using S = Smp<M>;
   constexpr int G = M::G;
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) {  // moment-update slot table (before any exit)
+    S::ik_fill();
+    __syncthreads();
+  }
   const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
   if (c >= A.K) return;  // whole lane groups exit together
   Grp<G> g;
