@@ -797,8 +797,8 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     HIPCHK(e, dalloc(&e->lg_itc, (size_t)K));
     HIPCHK(e, dalloc(&e->lg_frames, (size_t)K * NutsFrames<MMB_LG_DV>::DBL));
     HIPCHK(e, dalloc(&e->lg_pos, (size_t)K * MMB_LG_DV));
-    HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NG * K * MMB_LG_DV));
-    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * K));
+    HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NG * MMB_LG_NS * K * MMB_LG_DV));
+    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * MMB_LG_NS * K));
     HIPCHK(e, dalloc(&e->lg_count, 2));
     HIPCHK(e, dalloc(&e->lg_ngrad, 1));
     if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, sizeof(int32_t), 0));

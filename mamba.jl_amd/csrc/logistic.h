@@ -39,8 +39,8 @@ struct LgArgs {
   double* draws;           // [n_kept][p][K] or null
   // gradient exchange between the two kernels
   double* pos;             // [K][64] positions of the chains that requested a gradient (slot order)
-  double* gpart;           // [MMB_LG_NG][K][64] group partials
-  double* lpart;           // [MMB_LG_NG][K]
+  double* gpart;           // [MMB_LG_NG * MMB_LG_NS][K][64] sub-range partials (one workgroup each)
+  double* lpart;           // [MMB_LG_NG * MMB_LG_NS][K]
   int32_t* count;          // [2] requests in the current step (ping-pong by step parity)
   unsigned long long* ngrad;  // total gradient evaluations of the window
   unsigned long long* nstat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat)

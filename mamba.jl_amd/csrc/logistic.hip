@@ -8,8 +8,9 @@
 //   lp  = y .* eta - softplus(eta),  res = y - invlogit(eta)      (fused, registers)
 //   G   = X' * res                   (64 x N)·(N x slots), f64 MFMA, D regs of the first
 //                                    GEMM reused directly as B operands of the second
-// as MMB_LG_NG group partials; the next lg_ctl_kernel sums them in group order (no atomics:
-// the summation order is the mmb_math.h spec, restated by oracle/oracle.c).
+// as MMB_LG_NG x MMB_LG_NS sub-range partials; the next lg_ctl_kernel folds them per group and
+// sums the groups in order (no atomics: the summation order is the mmb_math.h spec, restated
+// by oracle/oracle.c).
 #include "hmc.h"
 #include "logistic.h"
 #include "nuts.h"
@@ -69,8 +70,15 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   const double x = S.x[0];
   const double sd2 = A.prior_sd * A.prior_sd;
   double gg = el ? -x / sd2 : 0.0;
+  // sub-range partials (one workgroup each) folded per group as ((P0 + P1) + P2) + .., then the
+  // group sums in group order: the summation spec of mmb_math.h
 #pragma unroll 4
-  for (int rg = 0; rg < MMB_LG_NG; ++rg) gg = gg + A.gpart[((size_t)rg * A.K + slot) * 64 + lane];
+  for (int rg = 0; rg < MMB_LG_NG; ++rg) {
+    double gs = A.gpart[((size_t)(rg * MMB_LG_NS) * A.K + slot) * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < MMB_LG_NS; ++w) gs = gs + A.gpart[((size_t)(rg * MMB_LG_NS + w) * A.K + slot) * 64 + lane];
+    gg = gg + gs;
+  }
   if (!isfinite(gg)) gg = 0.0;
   S.g[0] = el ? gg : 0.0;
   const bool bad = el && !isfinite(x);
@@ -79,7 +87,12 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   double lf = 0.0 + (__ballot(bad) ? -__builtin_inf() : d_iso(A.p, A.prior_sd, ssq));
   if (isfinite(lf)) {
     double ylp = 0.0;
-    for (int rg = 0; rg < MMB_LG_NG; ++rg) ylp = ylp + A.lpart[(size_t)rg * A.K + slot];
+    for (int rg = 0; rg < MMB_LG_NG; ++rg) {
+      double ls = A.lpart[(size_t)(rg * MMB_LG_NS) * A.K + slot];
+#pragma unroll
+      for (int w = 1; w < MMB_LG_NS; ++w) ls = ls + A.lpart[(size_t)(rg * MMB_LG_NS + w) * A.K + slot];
+      ylp = ylp + ls;
+    }
     lf = lf + ylp;
   }
   S.lf = lf;
@@ -166,6 +179,9 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
   if (blockIdx.x == 0 && threadIdx.x == 0) A.count[parity ^ 1] = 0;  // next step's counter
   const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (c >= A.K) return;
+  // a chain done with the window reads one word, not its whole machine (most chains at the
+  // end of a window)
+  if (!start && A.iv[(size_t)c * MMB_LG_NIV] == MC::IDLE) return;
   Grp<64> g;
   const int lane = g.lane;
   typename MC::St S;
@@ -202,12 +218,15 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
   }
 }
 
-// 1-D grid of MMB_LG_NG * ceil(K/64) workgroups of 4 waves.  Workgroup -> (group gi, 64-chain
-// tile ct): blocks are dealt round-robin over the 8 XCDs, so XCD x gets groups 2x and 2x+1
-// only and its L2 holds just those rows of X; tiles ascend with the block id, so the blocks
-// beyond the active count (the end of a window) are the last dispatched and exit at once.
-// Wave w owns chains ct*64 + 16w .. +15 (lane l: chain column l & 15, k-group l >> 4) and
-// walks the group's MMB_LG_NS sub-ranges in order, folding their partials as ((P0+P1)+P2)+.. in
+// 1-D grid of MMB_LG_NG * MMB_LG_NS * ceil(K/64) workgroups of 4 waves.  Workgroup -> (unit un =
+// group * MMB_LG_NS + sub-range, 64-chain tile ct): blocks are dealt round-robin over the 8 XCDs,
+// so XCD x gets units 8x .. 8x+7 (groups 4x .. 4x+3) only and its L2 holds just those rows of X;
+// tiles ascend with the block id, so the blocks beyond the active count (the end of a window)
+// are the last dispatched and exit at once.  One sub-range per workgroup: a step's latency is
+// one sub-range's passes (most steps at the end of a window carry few chains), and the ctl
+// kernel folds the MMB_LG_NS partials of a group as ((P0 + P1) + P2) + .. (the spec).
+// Wave w owns chains ct*64 + 16w .. +15 (lane l: chain column l & 15, k-group l >> 4) and walks
+// its sub-range's 32-row passes in order, accumulating in
 // registers (the summation spec the oracle restates).  The workgroup stages each 32-row
 // pass of X once in LDS for all 4 waves (4x fewer L2 reads per MFMA than per-wave loads,
 // which were the bottleneck: a 16x16x4 f64 MFMA issues every 64 cycles per SIMD and needs
@@ -230,10 +249,10 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
   const int nact = A.count[parity];
   if (blockIdx.x == 0 && threadIdx.x == 0 && nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
   const int b = (int)blockIdx.x;
-  constexpr int GPX = MMB_LG_NG / 8;  // groups per XCD
+  constexpr int UPX = MMB_LG_NG * MMB_LG_NS / 8;  // (group, sub-range) units per XCD
   const int idx = b >> 3;
-  const int gi = GPX * (b & 7) + idx % GPX;
-  const int ct = idx / GPX;
+  const int un = UPX * (b & 7) + idx % UPX;       // unit = gi * MMB_LG_NS + sub-range
+  const int ct = idx / UPX;
   if (ct * 64 >= nact) return;  // uniform over the workgroup
   const int tid = (int)threadIdx.x;
   const int w = tid >> 6;
@@ -262,9 +281,9 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
     }
     pfy = tid < nrows ? A.y[r0 + tid] : 0.0;
   };
-  fetch((gi * MMB_LG_NS) * rps, rps < LG_RB ? rps : LG_RB);
-  for (int s = 0; s < MMB_LG_NS; ++s) {
-    const int rbase = (gi * MMB_LG_NS + s) * rps;
+  fetch(un * rps, rps < LG_RB ? rps : LG_RB);
+  {
+    const int rbase = un * rps;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
     double lsum = 0.0;
@@ -278,9 +297,8 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
       __syncthreads();
       {  // prefetch the next pass (or the next sub-range's first) while this one computes
         int nr0 = r0 + LG_RB, nn = rps - (ps + 1) * LG_RB;
-        if (ps + 1 == npass) { nr0 = rbase + rps; nn = rps; }
         if (nn > LG_RB) nn = LG_RB;
-        if (!(ps + 1 == npass && s + 1 == MMB_LG_NS)) fetch(nr0, nn);
+        if (ps + 1 < npass) fetch(nr0, nn);
       }
       const bool two = nrows > 16;
       mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
@@ -327,24 +345,18 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
     }
     lsum = lsum + __shfl_xor(lsum, 16, 64);
     lsum = lsum + __shfl_xor(lsum, 32, 64);
-    if (s == 0) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) tot[mt] = acc[mt];
-      ltot = lsum;
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) tot[mt] = tot[mt] + acc[mt];
-      ltot = ltot + lsum;
-    }
+    for (int mt = 0; mt < 4; ++mt) tot[mt] = acc[mt];
+    ltot = lsum;
   }
   if (!live) return;
   // coefficient 16 mt + lq + 4 q of chain lc
-  double* gp = A.gpart + ((size_t)gi * A.K + slot) * 64;
+  double* gp = A.gpart + ((size_t)un * A.K + slot) * 64;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int q = 0; q < 4; ++q) gp[16 * mt + lq + 4 * q] = tot[mt][q];
-  if (lq == 0) A.lpart[(size_t)gi * A.K + slot] = ltot;
+  if (lq == 0) A.lpart[(size_t)un * A.K + slot] = ltot;
 }
 
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st) {
@@ -358,7 +370,7 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t
   return hipGetLastError();
 }
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {
-  const dim3 grid(MMB_LG_NG * ((A.K + 63) / 64)), blk(256);
+  const dim3 grid(MMB_LG_NG * MMB_LG_NS * ((A.K + 63) / 64)), blk(256);
   if (A.p <= 52)
     hipLaunchKernelGGL(lg_grad_kernel<13>, grid, blk, 0, st, A, parity);
   else
