@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 CHAINS_PER_GPU = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (spec, dense)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_rats_hbm_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_rats_gibbs_amm_hbm_traffic.json")
 
 
 def parse():
@@ -208,9 +208,10 @@ def setup_workload(mb, args, rank):
 
 
 def pmc_traffic(args, W):
-    """HBM bytes per sweep launch from the committed rocprofv3 PMC pass of this exact
-    kernel configuration (profiles/, gathered and corrected by tools/hbm_traffic.py as
-    MI355X_MICROARCH.md prescribes); None when no such pass matches."""
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC pass of this exact kernel
+    build and configuration (profiles/, gathered by tools/profiles_run.sh and corrected by
+    tools/profiles_pmc_summary.py as MI355X_MICROARCH.md prescribes; the library's sha256 must
+    match); None when no such pass matches."""
     if args.workload != "rats" or not os.path.exists(TRAFFIC_FILE):
         return None, None
     try:
@@ -219,6 +220,11 @@ def pmc_traffic(args, W):
         return None, None
     if (t.get("scheme"), t.get("chains"), t.get("iters_per_launch")) != (args.scheme, args.chains, W):
         return None, None
+    import hashlib
+    import _mamba_path
+    lib = _mamba_path.load().abi.LIB_PATH
+    if t.get("lib_sha256") != hashlib.sha256(open(lib, "rb").read()).hexdigest():
+        return None, None  # counters of another build of the kernel: not this run's traffic
     return t.get("bytes_per_launch"), os.path.relpath(TRAFFIC_FILE, ROOT)
 
 

@@ -5,7 +5,7 @@
 Writes <prefix>_sweep_summary.json (per-launch averages of the fused sweep kernel's PMC
 counters, the rocprofv3 --stats average and the average of the last `--last` launches,
 which are the event-timed roofline launches of bench.py), copies the kernel stats CSV
-and bench line, and writes profiles/hbm_traffic.json (HBM bytes per launch, corrected as
+and bench line, and writes <prefix>_hbm_traffic.json (HBM bytes per launch, corrected as
 MI355X_MICROARCH.md prescribes: FETCH_SIZE is KiB and reports half of wide coalesced
 reads on gfx950, so bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE).
 """
@@ -14,13 +14,17 @@ import csv
 import glob
 import json
 import os
+import hashlib
 import shutil
 
 ap = argparse.ArgumentParser()
 ap.add_argument("src")
 ap.add_argument("prefix")
-ap.add_argument("--last", type=int, default=8)
+ap.add_argument("--last", type=int, default=16)
+ap.add_argument("--scheme", default="gibbs_amm")
 a = ap.parse_args()
+# the engine build the counters were taken from (bench.py uses the traffic only for this build)
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mamba.jl_amd", "lib", "libmambahip.so")
 
 out = {}
 for f in sorted(glob.glob(os.path.join(a.src, "pmc_*", "run_counter_collection.csv"))):
@@ -28,7 +32,8 @@ for f in sorted(glob.glob(os.path.join(a.src, "pmc_*", "run_counter_collection.c
     for r in csv.DictReader(open(f)):
         if "sweep_kernel" in r["Kernel_Name"]:
             acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    for k, v in acc.items():
+    for k, v in acc.items():  # the last `--last` launches: bench.py's steady-state roofline window
+        v = v[-a.last:]
         out[k] = sum(v) / len(v)
         out[k + "_launches"] = len(v)
 st = os.path.join(a.src, "trace", "run_kernel_stats.csv")
@@ -55,10 +60,14 @@ if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
     hbm = 2 * 1024 * out["FETCH_SIZE"] + 1024 * out["WRITE_SIZE"]
     out["hbm_bytes_per_launch"] = hbm
     rd = os.path.dirname(os.path.abspath(a.prefix))
+    cfg = b["config"] if os.path.exists(bench) else {}
     json.dump({"bytes_per_launch": hbm, "source": os.path.basename(a.prefix) + "_sweep_summary.json",
-               "formula": "2*1024*FETCH_SIZE + 1024*WRITE_SIZE (KiB counters; gfx950 wide-read x2)",
-               "algorithmic_bytes_per_launch": out.get("algorithmic_bytes_per_launch")},
-              open(os.path.join(rd, "hbm_traffic.json"), "w"), indent=1)
+               "formula": "2*1024*FETCH_SIZE + 1024*WRITE_SIZE (KiB counters; gfx950 wide-read x2), "
+                          "averaged over the last %d launches (the bench's steady-state roofline window)" % a.last,
+               "algorithmic_bytes_per_launch": out.get("algorithmic_bytes_per_launch"),
+               "scheme": a.scheme, "chains": cfg.get("chains_per_gpu"), "iters_per_launch": cfg.get("iters_per_launch"),
+               "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()},
+              open(a.prefix + "_hbm_traffic.json", "w"), indent=1)
 if os.path.exists(st):
     shutil.copy(st, a.prefix + "_kernel_stats.csv")
 json.dump(out, open(a.prefix + "_sweep_summary.json", "w"), indent=1)
