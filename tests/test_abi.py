@@ -128,3 +128,15 @@ def test_comm_init_validates_before_touching_the_device(mamba):
     assert lib.mmb_range_allreduce(None, None) == -1
     assert lib.mmb_gr_allreduce(None, None, None, None) == -1
     lib.mmb_comm_destroy(None)
+
+
+def test_julia_shim_binds_declared_symbols():
+    """julia/MambaHIP.jl (the ccall shim, not runnable here) binds only entry points the
+    header declares and the library exports, and covers the ones a mcmc_master! branch needs."""
+    src = open(os.path.join(ROOT, "julia", "MambaHIP.jl")).read()
+    bound = set(re.findall(r"ccall\(\(:(mmb_\w+), libmambahip\)", src))
+    declared = set(declared_symbols())
+    assert bound and not (bound - declared), bound - declared
+    need = {"mmb_create", "mmb_set_data", "mmb_init_chains", "mmb_run", "mmb_get_values", "mmb_get_tune",
+            "mmb_set_tune", "mmb_set_iter", "mmb_comm_init", "mmb_gr_allreduce", "mmb_range_allreduce"}
+    assert need <= bound, need - bound
