@@ -24,8 +24,8 @@
 #include <rccl/rccl.h>
 
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
-hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st);
-hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st);
+hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, hipStream_t st);
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
                                hipStream_t st);
 hipError_t mmb_launch_chain_summary(int P, int64_t n, int K, int64_t kg0, int64_t bs, const double* draws,
@@ -76,8 +76,9 @@ struct mmb_engine {
   double *lg_X = nullptr, *lg_y = nullptr;
   double *lg_vec = nullptr, *lg_sc = nullptr, *lg_frames = nullptr, *lg_pos = nullptr;
   double *lg_gpart = nullptr, *lg_lpart = nullptr;
-  int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr;
+  int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr, *lg_s2c = nullptr;
   int64_t* lg_itc = nullptr;
+  hipEvent_t lg_cev[2] = {nullptr, nullptr};  // request-count readbacks in flight (run_logistic)
   int64_t lg_steps = 0;  // gradient steps of the last window
   unsigned long long* lg_ngrad = nullptr;
   unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum}, Slice overflows
@@ -499,11 +500,11 @@ static void free_dev(mmb_engine* e) {
   if (e->d_blocks) (void)hipFree(e->d_blocks);
   {
     void* lp[] = {e->lg_vec, e->lg_sc, e->lg_frames, e->lg_pos, e->lg_gpart, e->lg_lpart, e->lg_iv,
-                  e->lg_count, e->lg_itc};
+                  e->lg_count, e->lg_itc, e->lg_s2c};
     for (void* q : lp)
       if (q) (void)hipFree(q);
     e->lg_vec = e->lg_sc = e->lg_frames = e->lg_pos = e->lg_gpart = e->lg_lpart = nullptr;
-    e->lg_iv = e->lg_count = nullptr;
+    e->lg_iv = e->lg_count = e->lg_s2c = nullptr;
     e->lg_itc = nullptr;
     if (e->lg_ngrad) (void)hipFree(e->lg_ngrad);
     e->lg_ngrad = nullptr;
@@ -538,6 +539,8 @@ void mmb_destroy(mmb_engine* e) {
   if (e->lg_X) (void)hipFree(e->lg_X);
   if (e->lg_y) (void)hipFree(e->lg_y);
   if (e->lg_hcount) (void)hipHostFree(e->lg_hcount);
+  for (hipEvent_t ev : e->lg_cev)
+    if (ev) (void)hipEventDestroy(ev);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
@@ -800,8 +803,11 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NG * MMB_LG_NS * K * MMB_LG_DV));
     HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * MMB_LG_NS * K));
     HIPCHK(e, dalloc(&e->lg_count, 2));
+    HIPCHK(e, dalloc(&e->lg_s2c, (size_t)2 * K));
     HIPCHK(e, dalloc(&e->lg_ngrad, 1));
-    if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, sizeof(int32_t), 0));
+    if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, 2 * sizeof(int32_t), 0));
+    for (hipEvent_t& ev : e->lg_cev)
+      if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   }
   int rc = upload_blocks(e);
   if (rc) return rc;
@@ -861,8 +867,8 @@ static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
 }
 
 // Config-4 window: ctl / grad kernel pairs until no chain requests a gradient.  The
-// request count is read back every LG_CHECK steps (pinned host word); surplus pairs after
-// the last chain finished are no-ops (the grad kernel exits on count 0, idle chains return).
+// request count is read back every LG_CHECK steps (pinned host words, one check behind the
+// launches); surplus pairs after the last chain finished are no-ops (the grad kernel exits on count 0, idle chains return).
 static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int64_t kept0, int64_t nk,
                         bool want) {
   constexpr int LG_CHECK = 8;
@@ -885,7 +891,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.tune = A.kind == MMB_SAMPLER_NUTS ? h.nuts : h.hmc;
   A.sigl = h.sigl_d;
   A.draws = draws;
-  A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count;
+  A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count; A.s2c = e->lg_s2c;
   A.ngrad = e->lg_ngrad;
   A.nstat = e->d_nstat;
   HIPCHK(e, hipMemsetAsync(e->lg_ngrad, 0, sizeof(unsigned long long), e->stream));
@@ -909,9 +915,10 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
     const int64_t cap = a->iters * per + extra + 4 * LG_CHECK;
     std::vector<hipEvent_t>& ev = e->evpool;
     HIPCHK(e, hipMemsetAsync(e->lg_count, 0, 2 * sizeof(int32_t), e->stream));
-    hipError_t st = mmb_lg_launch_ctl(A, 1, 0, e->stream);
+    hipError_t st = mmb_lg_launch_ctl(A, 1, 0, (int)e->K, e->stream);
     if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
     int64_t s = 0;
+    int nbound = (int)e->K;  // running chains, as last read back (non-increasing in a window)
     for (;;) {
       const int par = (int)(s & 1);
       if (a->time_kernels) {
@@ -922,17 +929,25 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
         }
         HIPCHK(e, hipEventRecord(ev[2 * s], e->stream));
       }
-      st = mmb_lg_launch_grad(A, par, e->stream);
+      st = mmb_lg_launch_grad(A, par, nbound, e->stream);
       if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_grad launch: %s", hipGetErrorString(st));
       if (a->time_kernels) HIPCHK(e, hipEventRecord(ev[2 * s + 1], e->stream));
-      st = mmb_lg_launch_ctl(A, 0, par ^ 1, e->stream);
+      st = mmb_lg_launch_ctl(A, 0, par ^ 1, nbound, e->stream);
       if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
       ++s;
       if (s % LG_CHECK == 0) {
-        HIPCHK(e, hipMemcpyAsync(e->lg_hcount, e->lg_count + (s & 1), sizeof(int32_t), hipMemcpyDeviceToHost,
-                                 e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        if (*e->lg_hcount == 0) break;
+        // two readbacks in flight: wait for the one issued LG_CHECK steps ago, so the
+        // stream still holds LG_CHECK queued steps while the host decides (the count is
+        // non-increasing, so the older value is still a bound on the running chains)
+        const int j = (int)((s / LG_CHECK) & 1);
+        HIPCHK(e, hipMemcpyAsync(e->lg_hcount + j, e->lg_count + (s & 1), sizeof(int32_t),
+                                 hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipEventRecord(e->lg_cev[j], e->stream));
+        if (s >= 2 * LG_CHECK) {
+          HIPCHK(e, hipEventSynchronize(e->lg_cev[j ^ 1]));
+          if (e->lg_hcount[j ^ 1] == 0) break;
+          nbound = e->lg_hcount[j ^ 1];
+        }
       }
       if (s > cap) return fail(e, MMB_E_STATE, "logistic window did not terminate");
     }

@@ -42,6 +42,9 @@ struct LgArgs {
   double* gpart;           // [MMB_LG_NG * MMB_LG_NS][K][64] sub-range partials (one workgroup each)
   double* lpart;           // [MMB_LG_NG * MMB_LG_NS][K]
   int32_t* count;          // [2] requests in the current step (ping-pong by step parity)
+  int32_t* s2c;            // [2][K] requesting chain of each slot (ping-pong): the next control
+                           //        kernel visits exactly these chains (every running chain
+                           //        requests one gradient per step)
   unsigned long long* ngrad;  // total gradient evaluations of the window
   unsigned long long* nstat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat)
 };

@@ -5,7 +5,8 @@
 // pos[slot] (slot = atomic counter; a chain's arithmetic does not depend on its slot);
 // lg_grad_kernel(parity) evaluates, for all requested slots,
 //   eta = X * B                      (N x 64)·(64 x slots), f64 MFMA 16x16x4
-//   lp  = y .* eta - softplus(eta),  res = y - invlogit(eta)      (fused, registers)
+//   lp  = y .* eta - softplus(eta),  res = y - invlogit(eta)      (fused, registers; the
+//         log(1 + exp(-|eta|)) terms as one product per lane and one log at the end)
 //   G   = X' * res                   (64 x N)·(N x slots), f64 MFMA, D regs of the first
 //                                    GEMM reused directly as B operands of the second
 // as MMB_LG_NG x MMB_LG_NS sub-range partials; the next lg_ctl_kernel folds them per group and
@@ -71,13 +72,21 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   const double sd2 = A.prior_sd * A.prior_sd;
   double gg = el ? -x / sd2 : 0.0;
   // sub-range partials (one workgroup each) folded per group as ((P0 + P1) + P2) + .., then the
-  // group sums in group order: the summation spec of mmb_math.h
-#pragma unroll 4
-  for (int rg = 0; rg < MMB_LG_NG; ++rg) {
-    double gs = A.gpart[((size_t)(rg * MMB_LG_NS) * A.K + slot) * 64 + lane];
+  // group sums in group order: the summation spec of mmb_math.h.  Loads are issued LG_AB groups
+  // at a time ahead of the adds (fewer dependent round trips, bounded registers).
+  constexpr int LG_AB = 8;
+  const double* gp = A.gpart + (size_t)slot * 64 + lane;
+  for (int r0 = 0; r0 < MMB_LG_NG; r0 += LG_AB) {
+    double gv[LG_AB * MMB_LG_NS];
 #pragma unroll
-    for (int w = 1; w < MMB_LG_NS; ++w) gs = gs + A.gpart[((size_t)(rg * MMB_LG_NS + w) * A.K + slot) * 64 + lane];
-    gg = gg + gs;
+    for (int u = 0; u < LG_AB * MMB_LG_NS; ++u) gv[u] = gp[(size_t)(r0 * MMB_LG_NS + u) * A.K * 64];
+#pragma unroll
+    for (int rg = 0; rg < LG_AB; ++rg) {
+      double gs = gv[rg * MMB_LG_NS];
+#pragma unroll
+      for (int w = 1; w < MMB_LG_NS; ++w) gs = gs + gv[rg * MMB_LG_NS + w];
+      gg = gg + gs;
+    }
   }
   if (!isfinite(gg)) gg = 0.0;
   S.g[0] = el ? gg : 0.0;
@@ -87,11 +96,17 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   double lf = 0.0 + (__ballot(bad) ? -__builtin_inf() : d_iso(A.p, A.prior_sd, ssq));
   if (isfinite(lf)) {
     double ylp = 0.0;
-    for (int rg = 0; rg < MMB_LG_NG; ++rg) {
-      double ls = A.lpart[(size_t)(rg * MMB_LG_NS) * A.K + slot];
+    for (int r0 = 0; r0 < MMB_LG_NG; r0 += LG_AB) {
+      double lv[LG_AB * MMB_LG_NS];
 #pragma unroll
-      for (int w = 1; w < MMB_LG_NS; ++w) ls = ls + A.lpart[(size_t)(rg * MMB_LG_NS + w) * A.K + slot];
-      ylp = ylp + ls;
+      for (int u = 0; u < LG_AB * MMB_LG_NS; ++u) lv[u] = A.lpart[(size_t)(r0 * MMB_LG_NS + u) * A.K + slot];
+#pragma unroll
+      for (int rg = 0; rg < LG_AB; ++rg) {
+        double ls = lv[rg * MMB_LG_NS];
+#pragma unroll
+        for (int w = 1; w < MMB_LG_NS; ++w) ls = ls + lv[rg * MMB_LG_NS + w];
+        ylp = ylp + ls;
+      }
     }
     lf = lf + ylp;
   }
@@ -176,12 +191,18 @@ struct LgHmc {
 
 template <class MC>
 __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) A.count[parity ^ 1] = 0;  // next step's counter
-  const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (c >= A.K) return;
-  // a chain done with the window reads one word, not its whole machine (most chains at the
-  // end of a window)
-  if (!start && A.iv[(size_t)c * MMB_LG_NIV] == MC::IDLE) return;
+  // the first step visits every chain; later steps visit the chains that requested the
+  // gradient just computed (slot order of the previous control kernel), so the grid and the
+  // work shrink with the running chains at the end of a window
+  const int si = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+  int c;
+  if (start) {
+    if (si >= A.K) return;
+    c = si;
+  } else {
+    if (si >= A.count[parity ^ 1]) return;
+    c = A.s2c[(size_t)(parity ^ 1) * A.K + si];
+  }
   Grp<64> g;
   const int lane = g.lane;
   typename MC::St S;
@@ -198,7 +219,10 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
     const int64_t cur = itc + 1;
     if (MC::advance(A, S, c, chain, cur, lane, g)) {
       int slot = 0;
-      if (lane == 0) slot = atomicAdd(&A.count[parity], 1);
+      if (lane == 0) {
+        slot = atomicAdd(&A.count[parity], 1);
+        A.s2c[(size_t)parity * A.K + slot] = c;
+      }
       slot = __shfl(slot, 0, 64);
       A.pos[(size_t)slot * 64 + lane] = S.x[0];
       MC::store(A, c, lane, S, slot, itc);
@@ -247,7 +271,10 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
   __shared__ __attribute__((aligned(16))) double xs[LG_RB][LG_LD];
   __shared__ double ys[LG_RB];
   const int nact = A.count[parity];
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
+    A.count[parity ^ 1] = 0;  // the next control kernel's counter (its input list was read before)
+  }
   const int b = (int)blockIdx.x;
   constexpr int UPX = MMB_LG_NG * MMB_LG_NS / 8;  // (group, sub-range) units per XCD
   const int idx = b >> 3;
@@ -286,7 +313,8 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
     const int rbase = un * rps;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
-    double lsum = 0.0;
+    double lsum = 0.0, lprod = 1.0;
+    int lexp = 0;
     for (int ps = 0; ps < npass; ++ps) {
       const int r0 = rbase + ps * LG_RB;
       const int nrows = rps - ps * LG_RB < LG_RB ? rps - ps * LG_RB : LG_RB;  // 16 or 32
@@ -313,27 +341,33 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
         for (int kk = 0; kk < KS; ++kk)
           eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
       }
-      // residual terms of both blocks first (branch-free: padded rows have X = 0, eta = 0,
-      // and are masked by a select), so the scheduler can overlap block 1's VALU work with
-      // block 0's X'*res MFMAs; sums keep the row order of the spec
-      double sres[2][4], lps[2][4];
+      // residual terms of both blocks first (branch-free), so the scheduler can overlap block 1's VALU work with
+      // block 0's X'*res MFMAs; the lane's lin sum and (1 + t) product keep the row order of
+      // the spec (mmb_math.h mmb_logistic_row)
+      double sres[2][4], lins[2][4], fac[2][4];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const mmb_d4 eta = h ? eta1 : eta0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = r0 + 16 * h + lq + 4 * i;
-          double lp, res;
-          mmb_logistic_terms(eta[i], ys[16 * h + lq + 4 * i], &lp, &res);
+          double lin, a, res;
+          mmb_logistic_row(eta[i], ys[16 * h + lq + 4 * i], &lin, &a, &res);
+          // padded rows (>= N, or the empty second block of a 16-row pass) have X = 0 and
+          // y = 0, so eta = 0, lin = +0 and X' res adds exact zeros: only the factor is masked
           const bool in = row < A.N && (h == 0 || two);
-          lps[h][i] = in ? lp : 0.0;
-          sres[h][i] = in ? res : 0.0;
+          lins[h][i] = lin;
+          fac[h][i] = in ? a : 1.0;
+          sres[h][i] = res;
         }
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) lsum = lsum + lps[h][i];
+        for (int i = 0; i < 4; ++i) {
+          lsum = lsum + lins[h][i];
+          lprod = lprod * fac[h][i];
+        }
         if (h == 1 && !two) break;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -342,7 +376,9 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
             acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 * h + 4 * i + lq][16 * mt + lc], sres[h][i], acc[mt],
                                                            0, 0, 0);
       }
+      mmb_lg_renorm(&lprod, &lexp);  // < 2^9 before: never overflows
     }
+    lsum = mmb_lg_lane_lp(lsum, lprod, lexp);
     lsum = lsum + __shfl_xor(lsum, 16, 64);
     lsum = lsum + __shfl_xor(lsum, 32, 64);
 #pragma unroll
@@ -359,8 +395,10 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
   if (lq == 0) A.lpart[(size_t)un * A.K + slot] = ltot;
 }
 
-hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t st) {
-  const dim3 grid((A.K + 3) / 4), blk(256);
+// nbound: an upper bound of the chains still running (the host's last read of the request
+// count; requests never increase within a window)
+hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, hipStream_t st) {
+  const dim3 grid(((start ? A.K : nbound) + 3) / 4), blk(256);
   if (A.kind == MMB_SAMPLER_HMC)
     hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<false>>, grid, blk, 0, st, A, start, parity);
   else if (A.kind == MMB_SAMPLER_MALA)
@@ -369,8 +407,8 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, hipStream_t
     hipLaunchKernelGGL(lg_ctl_kernel<LgNuts>, grid, blk, 0, st, A, start, parity);
   return hipGetLastError();
 }
-hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, hipStream_t st) {
-  const dim3 grid(MMB_LG_NG * MMB_LG_NS * ((A.K + 63) / 64)), blk(256);
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, hipStream_t st) {
+  const dim3 grid(MMB_LG_NG * MMB_LG_NS * ((nbound + 63) / 64)), blk(256);
   if (A.p <= 52)
     hipLaunchKernelGGL(lg_grad_kernel<13>, grid, blk, 0, st, A, parity);
   else

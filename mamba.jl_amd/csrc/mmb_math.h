@@ -338,49 +338,41 @@ MMB_HD double mmb_exp_neg(double x) {
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  const int64_t k = (int64_t)kd;                          /* -1075 .. 0 */
-  const double big = mmb_u2d(mmb_d2u(p) + ((uint64_t)k << 52));
-  const double small = mmb_u2d(mmb_d2u(p) + ((uint64_t)(k + 1000) << 52)) * 9.33263618503218878990e-302;
+  const int32_t k = (int32_t)kd;                          /* -1075 .. 0 */
+  const double big = mmb_u2d(mmb_d2u(p) + ((uint64_t)(int64_t)k << 52));
+  const double small = mmb_u2d(mmb_d2u(p) + ((uint64_t)(int64_t)(k + 1000) << 52)) * 9.33263618503218878990e-302;
   const double e = k >= -1021 ? big : small;
-  return x > -745.2 ? e : (x != x ? x : 0.0);
+  const double z = x > -745.2 ? e : 0.0 * e; /* e used on both sides: the compiler keeps it branch-free */
+  return x != x ? x : z;
 }
 
-/* log1p(t) for t in [0, 1]: 2 atanh(s), s = t / (2 + t) <= 1/3, as the odd series
- * 2 s sum_k s^(2k) / (2k + 1) to k = 16 (truncation < 2^-56); one division, no branches. */
-/* 2 atanh(s) = log((1 + s) / (1 - s)) for 0 <= s <= 1/3: the odd series to s^33 in Horner form */
-MMB_HD double mmb_atanh2_series(double s) {
-  const double z = s * s;
-  double p = 1.0 / 33.0;
-  p = fma(p, z, 1.0 / 31.0);
-  p = fma(p, z, 1.0 / 29.0);
-  p = fma(p, z, 1.0 / 27.0);
-  p = fma(p, z, 1.0 / 25.0);
-  p = fma(p, z, 1.0 / 23.0);
-  p = fma(p, z, 1.0 / 21.0);
-  p = fma(p, z, 1.0 / 19.0);
-  p = fma(p, z, 1.0 / 17.0);
-  p = fma(p, z, 1.0 / 15.0);
-  p = fma(p, z, 1.0 / 13.0);
-  p = fma(p, z, 1.0 / 11.0);
-  p = fma(p, z, 1.0 / 9.0);
-  p = fma(p, z, 1.0 / 7.0);
-  p = fma(p, z, 1.0 / 5.0);
-  p = fma(p, z, 1.0 / 3.0);
-  const double s2 = 2.0 * s;
-  return fma(s2, z * p, s2);
-}
-MMB_HD double mmb_log1p_unit(double t) { return mmb_atanh2_series(t / (2.0 + t)); }
-
-MMB_HD void mmb_logistic_terms(double eta, double y, double* lp, double* res) {
-  /* one IEEE division shared by both quotients: R = 1/((1+t)(2+t)), 1/(1+t) = (2+t) R,
-   * t/(2+t) = t (1+t) R (a few ulp instead of correctly rounded; host and device agree) */
+/* Per-row terms of the logistic likelihood: t = exp(-|eta|), a = 1 + t, R = 1/a (one IEEE
+ * division);  lin = y*eta - max(eta, 0),  lp = lin - log(a)  (so lp = y*eta - softplus(eta)),
+ * res = y - invlogit(eta) = y - (eta >= 0 ? R : t R).
+ * The log(a) terms are not taken per row: a lane multiplies its rows' factors a (each in
+ * [1, 2]) into P * 2^E and takes one log at the end (mmb_lg_lane_lp).  Renormalising P is a
+ * scaling by a power of two, exact in the normal range, so the product's value does not
+ * depend on when it is renormalised -- only on the multiplication order (the spec). */
+MMB_HD void mmb_logistic_row(double eta, double y, double* lin, double* a, double* res) {
   const double t = mmb_exp_neg(-fabs(eta));
-  const double a = 1.0 + t, b = 2.0 + t;
-  const double R = 1.0 / (a * b);
-  const double sp = (eta > 0.0 ? eta : 0.0) + mmb_atanh2_series((t * a) * R);
-  *lp = y * eta - sp;
-  const double q = b * R;
-  *res = y - (eta >= 0.0 ? q : t * q);
+  const double aa = 1.0 + t;
+  const double R = 1.0 / aa;
+  *lin = y * eta - (eta > 0.0 ? eta : 0.0);
+  *a = aa;
+  *res = y - (eta >= 0.0 ? R : t * R);
+}
+/* P = m 2^e (finite, >= 1) -> P = m in [1, 2), E += e; NaN / inf stay as they are */
+MMB_HD void mmb_lg_renorm(double* P, int* E) {
+  const uint64_t u = mmb_d2u(*P);
+  const int ex = (int)((u >> 52) & 0x7ff);
+  const int fin = ex != 0x7ff;
+  *E += fin ? ex - 1023 : 0;
+  *P = fin ? mmb_u2d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull) : *P;
+}
+/* a lane's lp partial: (sum of its lin) - log(product of its a) */
+MMB_HD double mmb_lg_lane_lp(double A, double P, int E) {
+  mmb_lg_renorm(&P, &E);
+  return A - (mmb_log(P) + (double)E * 6.93147180559945286227e-01);
 }
 
 #endif /* MMB_MATH_H */

@@ -37,11 +37,13 @@ class Oracle:
         L.orc_block_logpdf_grad.restype = C.c_double
         L.orc_block_logpdf_grad.argtypes = [P, DD, C.POINTER(I64), D, C.c_int, D, D]
         L.orc_pivoted_cholesky.argtypes = [C.c_int, D, D, C.POINTER(C.c_int)]
-        for f in ("orc_log", "orc_exp", "orc_log1p", "orc_exp_neg", "orc_log1p_unit"):
+        for f in ("orc_log", "orc_exp", "orc_log1p", "orc_exp_neg"):
             getattr(L, f).restype = C.c_double
             getattr(L, f).argtypes = [C.c_double]
         L.orc_sincos2pi.argtypes = [C.c_double, D, D]
-        L.orc_logistic_terms.argtypes = [C.c_double, C.c_double, D, D]
+        L.orc_logistic_row.argtypes = [C.c_double, C.c_double, D, D, D]
+        L.orc_lg_lane_lp.restype = C.c_double
+        L.orc_lg_lane_lp.argtypes = [C.c_double, C.c_double, C.c_int]
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32)] * 3
         for f in ("orc_uniform", "orc_normal"):
             getattr(L, f).restype = C.c_double

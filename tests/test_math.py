@@ -34,8 +34,6 @@ def ulps(a, b):
     ("orc_log1p", np.log1p, lambda r: np.exp(r.uniform(-40, 3, 20000))),
     ("orc_exp_neg", np.exp, lambda r: r.uniform(-745, 0, 20000)),
     ("orc_exp_neg", np.exp, lambda r: -np.exp(r.uniform(-60, 0, 20000))),
-    ("orc_log1p_unit", np.log1p, lambda r: r.uniform(0, 1, 20000)),
-    ("orc_log1p_unit", np.log1p, lambda r: np.exp(r.uniform(-745, 0, 20000))),
 ])
 def test_elementary_within_one_ulp(oracle, fn, npf, gen):
     x = gen(np.random.default_rng(7))
@@ -43,7 +41,7 @@ def test_elementary_within_one_ulp(oracle, fn, npf, gen):
     got = np.array([f(float(v)) for v in x])
     ref = npf(x)
     bad = ulps(got, ref)
-    tol = 2 if fn in ("orc_log1p", "orc_log1p_unit") else 1
+    tol = 2 if fn == "orc_log1p" else 1
     assert bad.max() <= tol, (x[bad.argmax()], got[bad.argmax()], ref[bad.argmax()])
 
 
@@ -56,7 +54,6 @@ def test_elementary_special_values(oracle):
     # logistic-term kernels (x <= 0, t in [0, 1])
     assert L.orc_exp_neg(0.0) == 1.0 and L.orc_exp_neg(-800.0) == 0.0 and L.orc_exp_neg(-np.inf) == 0.0
     assert np.isnan(L.orc_exp_neg(np.nan)) and L.orc_exp_neg(-745.1) == 5e-324
-    assert L.orc_log1p_unit(0.0) == 0.0 and L.orc_log1p_unit(1e-300) == 1e-300
     assert abs(L.orc_log(5e-324) - np.log(5e-324)) < 1e-12  # subnormal path
 
 
@@ -94,28 +91,55 @@ def test_gamma_marsaglia_tsang(oracle, a):
     assert abs(g.var() / a - 1) < 0.06
 
 
-def test_logistic_terms_accuracy(oracle):
-    """mmb_logistic_terms (config-4 per-row terms, one shared division): lp = y*eta -
-    softplus(eta) and res = y - invlogit(eta) against an 80-bit long-double evaluation."""
+def test_logistic_row_accuracy(oracle):
+    """mmb_logistic_row (config-4 per-row terms): lin = y*eta - max(eta, 0), a = 1 + exp(-|eta|)
+    and res = y - invlogit(eta), against an 80-bit long-double evaluation; lp = lin - log(a)
+    (taken once per lane through mmb_lg_lane_lp)."""
     import ctypes as C
     r = np.random.default_rng(11)
     eta = np.concatenate([r.normal(0, 3, 20000), r.uniform(-745, 745, 2000), [0.0, -0.0, 1e-300, -1e-300, 40.0, -40.0]])
-    lp1, rs1, lp0, rs0 = (np.empty(eta.size) for _ in range(4))
-    a, b = C.c_double(), C.c_double()
-    for k, e in enumerate(eta):
-        oracle.L.orc_logistic_terms(float(e), 1.0, C.byref(a), C.byref(b))
-        lp1[k], rs1[k] = a.value, b.value
-        oracle.L.orc_logistic_terms(float(e), 0.0, C.byref(a), C.byref(b))
-        lp0[k], rs0[k] = a.value, b.value
+    out = {y: [np.empty(eta.size) for _ in range(4)] for y in (0.0, 1.0)}
+    lin, a, rs = C.c_double(), C.c_double(), C.c_double()
+    for y in (0.0, 1.0):
+        o = out[y]
+        for k, e in enumerate(eta):
+            oracle.L.orc_logistic_row(float(e), y, C.byref(lin), C.byref(a), C.byref(rs))
+            o[0][k], o[1][k], o[2][k] = lin.value, a.value, rs.value
+            o[3][k] = oracle.L.orc_lg_lane_lp(lin.value, a.value, 0)
     E = eta.astype(np.longdouble)
     t = np.exp(-np.abs(E))
     sp = np.maximum(E, 0) + np.log1p(t)
     sig = np.where(E >= 0, 1 / (1 + t), t / (1 + t))
-    for got, ref in ((lp1, E - sp), (lp0, -sp)):
-        ref = ref.astype(np.float64)
-        # y*eta - softplus(eta) cancels for large |eta|: scale by max(|lp|, |eta|) (measured 5.1e-16 * scale)
-        scale = np.maximum(np.maximum(np.abs(ref), np.abs(eta)), 1e-300)
-        assert (np.abs(got - ref) / scale).max() <= 8e-16
-    # residuals: absolute error (they are the score terms summed into the gradient)
-    assert np.abs(rs1 - (1 - sig).astype(np.float64)).max() <= 4.5e-16
-    assert np.abs(rs0 - (-sig).astype(np.float64)).max() <= 4.5e-16
+    for y in (0.0, 1.0):
+        got_lin, got_a, got_res, got_lp = out[y]
+        assert np.array_equal(got_lin, (y * eta - np.maximum(eta, 0)))
+        assert np.abs(got_a - (1 + t).astype(np.float64)).max() <= 2.3e-16
+        ref = (y * E - sp).astype(np.float64)
+        # absolute error of the per-row lp (a = 1 + t rounds t below 2^-53 away; the row terms
+        # are summed, so absolute error is the measure): <= 2^-52 relative to max(|lp|, 1)
+        assert (np.abs(got_lp - ref) / np.maximum(np.abs(ref), 1.0)).max() <= 4.5e-16
+        assert np.abs(got_res - (y - sig).astype(np.float64)).max() <= 2.3e-16
+
+
+def test_lane_product_renormalisation_is_exact(oracle):
+    """The lane product P 2^E of the (1 + t) factors does not depend on when it is renormalised
+    (power-of-two scaling is exact): log of a 4000-factor product (overflows without it)."""
+    import ctypes as C
+    r = np.random.default_rng(5)
+    f = 1.0 + r.uniform(0, 1, 4000)
+    P, E = 1.0, 0
+    for v in f:
+        P = P * v
+        m, e = np.frexp(P)          # P = m 2^e, m in [0.5, 1)
+        P, E = m * 2.0, E + int(e) - 1
+    got = oracle.L.orc_lg_lane_lp(0.0, P, E)
+    ref = -float(np.sum(np.log(f.astype(np.longdouble))))
+    assert abs(got - ref) <= 1e-9 * abs(ref)
+    # every fourth factor instead of every factor: the same bits
+    P2, E2 = 1.0, 0
+    for k, v in enumerate(f):
+        P2 = P2 * v
+        if k % 4 == 3:
+            m, e = np.frexp(P2)
+            P2, E2 = m * 2.0, E2 + int(e) - 1
+    assert oracle.L.orc_lg_lane_lp(0.0, P2, E2) == got
