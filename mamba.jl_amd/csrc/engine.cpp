@@ -368,7 +368,11 @@ static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int d
            (v.empty() || hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess);
     };
     up(&e->d_ir_nodes, e->ir_nodes);
-    up(&e->d_ir_code, e->ir_code);
+    {  // padded with END words: the interpreter fetches one word ahead (ir.h ev)
+      std::vector<int32_t> code(e->ir_code);
+      code.resize(code.size() + 2, 0);
+      up(&e->d_ir_code, code);
+    }
     up(&e->d_ir_const, e->ir_const);
     up(&e->d_ir_pool, e->ir_pool);
     up(&e->d_ir_mon, e->ir_mon);

@@ -451,3 +451,26 @@ def test_gr_allreduce_rccl_one_gpu(mamba, how):
     shift = np.array([3.6, 6.0, 100.0])
     np.testing.assert_array_equal(comm.gr_allreduce(kinds, shift), eng.gr_partials(kinds, shift))
     comm.close()
+
+
+def test_rats_scale_total_on_one_gpu(mamba, oracle):
+    """The 8-GPU configuration's 131 072 chains (8 x 16 384, BASELINE configs[4]) in ONE engine:
+    rank 5's shard run alone (its chain range, chain_offset = 5 x 16 384) reproduces its
+    columns bit for bit -- a chain's draws depend only on its global id, so the weak-scaling
+    shards of bench.py compute exactly the single-engine result -- and the first chains
+    match the oracle."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    K, S, r = 131072, 16384, 5
+    init = mamba.model.rats_init_ls(K, seed=21)
+    e = mamba.Engine(m)
+    e.init_chains(init, seed=8)
+    d = e.run(24, burnin=0, thin=4)
+    assert d.shape == (6, 3, K) and np.isfinite(d).all()
+    vals = e.values()
+    e5 = mamba.Engine(m)
+    e5.init_chains(init[r * S:(r + 1) * S], chain_offset=r * S, seed=8)
+    np.testing.assert_array_equal(e5.run(24, burnin=0, thin=4), d[:, :, r * S:(r + 1) * S])
+    np.testing.assert_array_equal(e5.values(), vals[r * S:(r + 1) * S])
+    st = oracle.new_state(m, init[:32])
+    do = oracle.run(m, st, 24, burnin=0, thin=4, seed=8, chain_offset=0, nthreads=8)
+    np.testing.assert_allclose(d[:, :, :32], do, rtol=1e-9, atol=1e-9)
