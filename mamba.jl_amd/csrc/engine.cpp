@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -186,6 +187,46 @@ int mmb_abi_version(void) { return MMB_ABI_VERSION; }
 const char* mmb_last_error(const mmb_engine* e) {
   if (e && !e->err.empty()) return e->err.c_str();
   return g_last_error.c_str();
+}
+
+// Device form of the node IR's expressions: a leaf immediately followed by a binary op
+// (postfix "... x leaf op") becomes one fused word MMB_IR_FUSED + 4 (leaf - 1) + (op - ADD)
+// with the leaf's argument (VALG keeps its second word): acc = acc op leaf instead of
+// spill, load, reload -- the same operands in the same order, so results are bit-identical
+// to the oracle, which interprets the unfused code.  Each distinct expression start is
+// rewritten once (validated code: every expression ends in END); node offsets are remapped.
+static void ir_fuse(const std::vector<int32_t>& code, std::vector<mmb_ir_node>& nodes, std::vector<int32_t>& out) {
+  std::map<int32_t, int32_t> start;
+  auto op_of = [&](size_t pc) { return (int)((uint32_t)code[pc] >> 24); };
+  for (mmb_ir_node& N : nodes)
+    for (int k = 0; k < 3; ++k) {
+      const int32_t s0 = N.expr[k];
+      if (s0 < 0) continue;
+      auto it = start.find(s0);
+      if (it == start.end()) {
+        const int32_t ns = (int32_t)out.size();
+        start[s0] = ns;
+        for (size_t pc = (size_t)s0;; ++pc) {
+          const int op = op_of(pc);
+          out.push_back(code[pc]);
+          if (op == MMB_IR_OP_END) break;
+          if (op >= 1 && op < 16) {
+            const size_t nx = pc + (op == MMB_IR_OP_VALG ? 2 : 1);
+            const int bo = op_of(nx);
+            if (bo >= MMB_IR_OP_ADD && bo <= MMB_IR_OP_DIV) {
+              out.back() = (int32_t)(((uint32_t)(MMB_IR_FUSED + 4 * (op - 1) + (bo - MMB_IR_OP_ADD)) << 24) |
+                                     ((uint32_t)code[pc] & 0xffffffu));
+              if (op == MMB_IR_OP_VALG) out.push_back(code[pc + 1]);
+              pc = nx;  // the binary op is folded in
+              continue;
+            }
+            if (op == MMB_IR_OP_VALG) out.push_back(code[++pc]);
+          }
+        }
+        it = start.find(s0);
+      }
+      N.expr[k] = it->second;
+    }
 }
 
 static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out) {
@@ -367,10 +408,13 @@ static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int d
       ok = hipMalloc((void**)dst, std::max<size_t>(v.size(), 1) * sizeof(T)) == hipSuccess &&
            (v.empty() || hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess);
     };
-    up(&e->d_ir_nodes, e->ir_nodes);
-    {  // padded with END words: the interpreter fetches one word ahead (ir.h ev)
-      std::vector<int32_t> code(e->ir_code);
+    {  // device code: every expression with its leaf+binop pairs fused (ir_fuse), padded
+       // with END words (the interpreter fetches one word ahead, ir.h ev)
+      std::vector<mmb_ir_node> nodes(e->ir_nodes);
+      std::vector<int32_t> code;
+      ir_fuse(e->ir_code, nodes, code);
       code.resize(code.size() + 2, 0);
+      up(&e->d_ir_nodes, nodes);
       up(&e->d_ir_code, code);
     }
     up(&e->d_ir_const, e->ir_const);

@@ -21,6 +21,10 @@
 #pragma once
 #include "device.h"
 
+// device-only opcodes: a leaf fused with the following binary op (engine.cpp ir_fuse),
+// MMB_IR_FUSED + 4 (leaf opcode - 1) + (binary opcode - MMB_IR_OP_ADD)
+#define MMB_IR_FUSED 64
+
 template <class T>
 __device__ __forceinline__ const T& ir_const_ref(const T* p, int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -79,23 +83,30 @@ struct Mdl<MMB_MODEL_IR> {
       int wn = ir_const_ref(A.ir_code, pc + 1);
       const int op = (int)((uint32_t)w >> 24), arg = w & 0xffffff;
       if (op == MMB_IR_OP_END) return acc;
-      if (op < 16) {
+      if (op < 16 || op >= MMB_IR_FUSED) {  // a leaf, pushed or (fused) combined with the top
+        const int lk = op < 16 ? op : ((op - MMB_IR_FUSED) >> 2) + 1;
         double v;
-        if (op == MMB_IR_OP_CONST) v = A.ir_const[arg];
-        else if (op == MMB_IR_OP_VAL) v = vals[arg];
-        else if (op == MMB_IR_OP_VALI) v = vals[arg + i];
-        else if (op == MMB_IR_OP_VALG) {  // two words: the gather's pool offset follows
+        if (lk == MMB_IR_OP_CONST) v = A.ir_const[arg];
+        else if (lk == MMB_IR_OP_VAL) v = vals[arg];
+        else if (lk == MMB_IR_OP_VALI) v = vals[arg + i];
+        else if (lk == MMB_IR_OP_VALG) {  // two words: the gather's pool offset follows
           ++pc;
           v = vals[arg + (int)A.ir_pool[wn + i]];
           wn = ir_const_ref(A.ir_code, pc + 1);
-        } else if (op == MMB_IR_OP_DATA) v = A.ir_pool[arg + i];
+        } else if (lk == MMB_IR_OP_DATA) v = A.ir_pool[arg + i];
         else v = A.ir_pool[arg];  // MMB_IR_OP_DATAS
-        // the bottom slot is never popped: no spill for an expression's first leaf (seeds
-        // 1.04e7 -> 1.095e7 /s; folding a leaf into a following binary op instead of the
-        // spill / reload measured slower, 1.025e7: the extra code-word load costs more)
-        if (sp > 0) stk[sp * G + lane] = acc;
-        ++sp;
-        acc = v;
+        if (op < 16) {
+          // the bottom slot is never popped: no spill for an expression's first leaf
+          if (sp > 0) stk[sp * G + lane] = acc;
+          ++sp;
+          acc = v;
+        } else {  // "leaf op" fused by the engine (engine.cpp ir_fuse): left = top, right = leaf
+          const int bo = (op - MMB_IR_FUSED) & 3;
+          if (bo == 0) acc = acc + v;
+          else if (bo == 1) acc = acc - v;
+          else if (bo == 2) acc = acc * v;
+          else acc = acc / v;
+        }
       } else if (op < 32) {
         --sp;
         const double l = stk[sp * G + lane];
