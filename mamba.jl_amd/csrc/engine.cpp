@@ -25,8 +25,8 @@
 #include <rccl/rccl.h>
 
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
-hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, hipStream_t st);
-hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, hipStream_t st);
+hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, int fold, hipStream_t st);
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, int fold, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
                                hipStream_t st);
 hipError_t mmb_launch_chain_summary(int P, int64_t n, int K, int64_t kg0, int64_t bs, const double* draws,
@@ -917,6 +917,9 @@ static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
 // Config-4 window: ctl / grad kernel pairs until no chain requests a gradient.  The
 // request count is read back every LG_CHECK steps (pinned host words, one check behind the
 // launches); surplus pairs after the last chain finished are no-ops (the grad kernel exits on count 0, idle chains return).
+#ifndef MMB_LG_FOLD_MIN
+#define MMB_LG_FOLD_MIN 1024  // chains: 16 tiles x 32 groups = 512 workgroups
+#endif
 static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int64_t kept0, int64_t nk,
                         bool want) {
   constexpr int LG_CHECK = 8;
@@ -963,7 +966,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
     const int64_t cap = a->iters * per + extra + 4 * LG_CHECK;
     std::vector<hipEvent_t>& ev = e->evpool;
     HIPCHK(e, hipMemsetAsync(e->lg_count, 0, 2 * sizeof(int32_t), e->stream));
-    hipError_t st = mmb_lg_launch_ctl(A, 1, 0, (int)e->K, e->stream);
+    hipError_t st = mmb_lg_launch_ctl(A, 1, 0, (int)e->K, 0, e->stream);
     if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
     int64_t s = 0;
     int nbound = (int)e->K;  // running chains, as last read back (non-increasing in a window)
@@ -977,10 +980,14 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
         }
         HIPCHK(e, hipEventRecord(ev[2 * s], e->stream));
       }
-      st = mmb_lg_launch_grad(A, par, nbound, e->stream);
+      // group mode once the step is wide enough to fill the GPU with one workgroup per
+      // (group, 64-chain tile): half the partial traffic; one workgroup per sub-range below
+      // that, where a step's latency is what counts
+      const int fold = nbound >= MMB_LG_FOLD_MIN ? 1 : 0;
+      st = mmb_lg_launch_grad(A, par, nbound, fold, e->stream);
       if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_grad launch: %s", hipGetErrorString(st));
       if (a->time_kernels) HIPCHK(e, hipEventRecord(ev[2 * s + 1], e->stream));
-      st = mmb_lg_launch_ctl(A, 0, par ^ 1, nbound, e->stream);
+      st = mmb_lg_launch_ctl(A, 0, par ^ 1, nbound, fold, e->stream);
       if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
       ++s;
       if (s % LG_CHECK == 0) {

@@ -65,26 +65,31 @@ __device__ __forceinline__ static void lg_store(const LgArgs& A, int c, int lane
 
 // logpdf!(m, x, block) and its gradient at S.x from the range partials (oracle logf_grad):
 // lf = 0 + prior, + sum of range partials if finite; grad = -x/sd^2 + partials, non-finite -> 0.
-template <class ST>
+// FOLD: the gradient kernel ran one workgroup per group and already formed each group's
+// ((P0 + P1) + ..) in unit slot group * MMB_LG_NS (lg_grad_kernel, fold mode); else the
+// MMB_LG_NS sub-range partials are folded here in the same order.
+template <bool FOLD, class ST>
 __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, int lane, const Grp<64>& g, ST& S) {
   const bool el = lane < A.p;
   const double x = S.x[0];
   const double sd2 = A.prior_sd * A.prior_sd;
   double gg = el ? -x / sd2 : 0.0;
-  // sub-range partials (one workgroup each) folded per group as ((P0 + P1) + P2) + .., then the
-  // group sums in group order: the summation spec of mmb_math.h.  Loads are issued LG_AB groups
-  // at a time ahead of the adds (fewer dependent round trips, bounded registers).
-  constexpr int LG_AB = 8;
+  // group sums added in group order: the summation spec of mmb_math.h.  Loads are issued 16
+  // partials at a time ahead of the adds (fewer dependent round trips, bounded registers).
+  constexpr int NW = FOLD ? 1 : MMB_LG_NS;  // partials read per group
+  constexpr int LG_AB = 16 / NW;            // groups per batch of loads
   const double* gp = A.gpart + (size_t)slot * 64 + lane;
   for (int r0 = 0; r0 < MMB_LG_NG; r0 += LG_AB) {
-    double gv[LG_AB * MMB_LG_NS];
+    double gv[LG_AB * NW];
 #pragma unroll
-    for (int u = 0; u < LG_AB * MMB_LG_NS; ++u) gv[u] = gp[(size_t)(r0 * MMB_LG_NS + u) * A.K * 64];
+    for (int rg = 0; rg < LG_AB; ++rg)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) gv[rg * NW + w] = gp[(size_t)((r0 + rg) * MMB_LG_NS + w) * A.K * 64];
 #pragma unroll
     for (int rg = 0; rg < LG_AB; ++rg) {
-      double gs = gv[rg * MMB_LG_NS];
+      double gs = gv[rg * NW];
 #pragma unroll
-      for (int w = 1; w < MMB_LG_NS; ++w) gs = gs + gv[rg * MMB_LG_NS + w];
+      for (int w = 1; w < NW; ++w) gs = gs + gv[rg * NW + w];
       gg = gg + gs;
     }
   }
@@ -97,14 +102,16 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   if (isfinite(lf)) {
     double ylp = 0.0;
     for (int r0 = 0; r0 < MMB_LG_NG; r0 += LG_AB) {
-      double lv[LG_AB * MMB_LG_NS];
+      double lv[LG_AB * NW];
 #pragma unroll
-      for (int u = 0; u < LG_AB * MMB_LG_NS; ++u) lv[u] = A.lpart[(size_t)(r0 * MMB_LG_NS + u) * A.K + slot];
+      for (int rg = 0; rg < LG_AB; ++rg)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) lv[rg * NW + w] = A.lpart[(size_t)((r0 + rg) * MMB_LG_NS + w) * A.K + slot];
 #pragma unroll
       for (int rg = 0; rg < LG_AB; ++rg) {
-        double ls = lv[rg * MMB_LG_NS];
+        double ls = lv[rg * NW];
 #pragma unroll
-        for (int w = 1; w < MMB_LG_NS; ++w) ls = ls + lv[rg * MMB_LG_NS + w];
+        for (int w = 1; w < NW; ++w) ls = ls + lv[rg * NW + w];
         ylp = ylp + ls;
       }
     }
@@ -190,7 +197,7 @@ struct LgHmc {
 };
 
 template <class MC>
-__global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity) {
+__global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity, int fold) {
   // the first step visits every chain; later steps visit the chains that requested the
   // gradient just computed (slot order of the previous control kernel), so the grid and the
   // work shrink with the running chains at the end of a window
@@ -213,7 +220,11 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
     itc = A.iter0;
   }
   if (S.pc == MC::IDLE) return;
-  if (MC::wants(S.pc)) lg_assemble(A, A.iv[(size_t)c * MMB_LG_NIV + 10], lane, g, S);
+  if (MC::wants(S.pc)) {
+    const int slot = A.iv[(size_t)c * MMB_LG_NIV + 10];
+    if (fold) lg_assemble<true>(A, slot, lane, g, S);
+    else lg_assemble<false>(A, slot, lane, g, S);
+  }
   const uint32_t chain = A.chain_offset + (uint32_t)c;
   for (;;) {
     const int64_t cur = itc + 1;
@@ -266,7 +277,11 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
 #define LG_PER (LG_RB * 64 / 256)  // doubles of a pass staged per thread
 // KS: MFMA k-steps of eta = X*B, ceil(p/4) rounded to 13 (p <= 52) or 16 (p <= MMB_LG_DV); the padded
 // coefficients are zero in X and in the positions, so both give the same sequential fma chain.
-template <int KS>
+// FOLD (wide steps, engine.cpp): one workgroup per (group, tile) walks the group's MMB_LG_NS
+// sub-ranges one after the other -- each its own fma chain from zero, as in the one-unit mode --
+// and writes the group's ((P0 + P1) + ..) to unit slot group * MMB_LG_NS: half the partials
+// written here and read by the control kernel, the same bits.
+template <int KS, bool FOLD>
 __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs A, int parity) {
   __shared__ __attribute__((aligned(16))) double xs[LG_RB][LG_LD];
   __shared__ double ys[LG_RB];
@@ -276,9 +291,10 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
     A.count[parity ^ 1] = 0;  // the next control kernel's counter (its input list was read before)
   }
   const int b = (int)blockIdx.x;
-  constexpr int UPX = MMB_LG_NG * MMB_LG_NS / 8;  // (group, sub-range) units per XCD
+  constexpr int NW = FOLD ? MMB_LG_NS : 1;                 // sub-ranges per workgroup
+  constexpr int UPX = MMB_LG_NG * MMB_LG_NS / (8 * NW);   // work units per XCD
   const int idx = b >> 3;
-  const int un = UPX * (b & 7) + idx % UPX;       // unit = gi * MMB_LG_NS + sub-range
+  const int un0 = (UPX * (b & 7) + idx % UPX) * NW;        // first sub-range: gi * MMB_LG_NS (+ w)
   const int ct = idx / UPX;
   if (ct * 64 >= nact) return;  // uniform over the workgroup
   const int tid = (int)threadIdx.x;
@@ -308,110 +324,127 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
     }
     pfy = tid < nrows ? A.y[r0 + tid] : 0.0;
   };
-  fetch(un * rps, rps < LG_RB ? rps : LG_RB);
-  {
-    const int rbase = un * rps;
+  fetch(un0 * rps, rps < LG_RB ? rps : LG_RB);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
-    double lsum = 0.0, lprod = 1.0;
-    int lexp = 0;
-    for (int ps = 0; ps < npass; ++ps) {
-      const int r0 = rbase + ps * LG_RB;
-      const int nrows = rps - ps * LG_RB < LG_RB ? rps - ps * LG_RB : LG_RB;  // 16 or 32
-      __syncthreads();  // previous pass's LDS reads are done
+  for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
+  double lsum = 0.0, lprod = 1.0;
+  int lexp = 0;
+  for (int q = 0; q < NW * npass; ++q) {
+    const int sw = NW == 1 ? 0 : q / npass, ps = NW == 1 ? q : q % npass;
+    const int r0 = (un0 + sw) * rps + ps * LG_RB;
+    const int nrows = rps - ps * LG_RB < LG_RB ? rps - ps * LG_RB : LG_RB;  // 16 or 32
+    __syncthreads();  // previous pass's LDS reads are done
 #pragma unroll
-      for (int e = 0; e < LG_PER; e += 2) *(double2*)&xs[srow][scol + e] = make_double2(pf[e], pf[e + 1]);
-      if (tid < LG_RB) ys[tid] = pfy;
-      __syncthreads();
-      {  // prefetch the next pass (or the next sub-range's first) while this one computes
-        int nr0 = r0 + LG_RB, nn = rps - (ps + 1) * LG_RB;
-        if (nn > LG_RB) nn = LG_RB;
-        if (ps + 1 < npass) fetch(nr0, nn);
+    for (int e = 0; e < LG_PER; e += 2) *(double2*)&xs[srow][scol + e] = make_double2(pf[e], pf[e + 1]);
+    if (tid < LG_RB) ys[tid] = pfy;
+    __syncthreads();
+    if (q + 1 < NW * npass) {  // prefetch the next pass (or the next sub-range's first) while this one computes
+      const int sw1 = NW == 1 ? 0 : (q + 1) / npass, ps1 = NW == 1 ? q + 1 : (q + 1) % npass;
+      int nn = rps - ps1 * LG_RB;
+      if (nn > LG_RB) nn = LG_RB;
+      fetch((un0 + sw1) * rps + ps1 * LG_RB, nn);
+    }
+    const bool two = nrows > 16;
+    mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
+    if (two) {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
+        eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 + lc][4 * kk + lq], bpos[kk], eta1, 0, 0, 0);
       }
-      const bool two = nrows > 16;
-      mmb_d4 eta0 = mmb_d4{0.0, 0.0, 0.0, 0.0}, eta1 = eta0;
-      if (two) {
+    } else {
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
-          eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 + lc][4 * kk + lq], bpos[kk], eta1, 0, 0, 0);
-        }
+      for (int kk = 0; kk < KS; ++kk)
+        eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
+    }
+    // residual terms of both blocks first (branch-free), so the scheduler can overlap block 1's
+    // VALU work with block 0's X'*res MFMAs; the lane's lin sum and (1 + t) product keep the
+    // row order of the spec (mmb_math.h mmb_logistic_row)
+    double sres[2][4], lins[2][4], fac[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const mmb_d4 eta = h ? eta1 : eta0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r0 + 16 * h + lq + 4 * i;
+        double lin, a, res;
+        mmb_logistic_row(eta[i], ys[16 * h + lq + 4 * i], &lin, &a, &res);
+        // padded rows (>= N, or the empty second block of a 16-row pass) have X = 0 and
+        // y = 0, so eta = 0, lin = +0 and X' res adds exact zeros: only the factor is masked
+        const bool in = row < A.N && (h == 0 || two);
+        lins[h][i] = lin;
+        fac[h][i] = in ? a : 1.0;
+        sres[h][i] = res;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lsum = lsum + lins[h][i];
+        lprod = lprod * fac[h][i];
+      }
+      if (h == 1 && !two) break;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 * h + 4 * i + lq][16 * mt + lc], sres[h][i], acc[mt],
+                                                         0, 0, 0);
+    }
+    mmb_lg_renorm(&lprod, &lexp);  // < 2^9 before: never overflows
+    if (ps == npass - 1) {  // end of a sub-range: its partials, folded into the group's in order
+      lsum = mmb_lg_lane_lp(lsum, lprod, lexp);
+      lsum = lsum + __shfl_xor(lsum, 16, 64);
+      lsum = lsum + __shfl_xor(lsum, 32, 64);
+      if (sw == 0) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) tot[mt] = acc[mt];
+        ltot = lsum;
       } else {
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk)
-          eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[lc][4 * kk + lq], bpos[kk], eta0, 0, 0, 0);
-      }
-      // residual terms of both blocks first (branch-free), so the scheduler can overlap block 1's VALU work with
-      // block 0's X'*res MFMAs; the lane's lin sum and (1 + t) product keep the row order of
-      // the spec (mmb_math.h mmb_logistic_row)
-      double sres[2][4], lins[2][4], fac[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const mmb_d4 eta = h ? eta1 : eta0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = r0 + 16 * h + lq + 4 * i;
-          double lin, a, res;
-          mmb_logistic_row(eta[i], ys[16 * h + lq + 4 * i], &lin, &a, &res);
-          // padded rows (>= N, or the empty second block of a 16-row pass) have X = 0 and
-          // y = 0, so eta = 0, lin = +0 and X' res adds exact zeros: only the factor is masked
-          const bool in = row < A.N && (h == 0 || two);
-          lins[h][i] = lin;
-          fac[h][i] = in ? a : 1.0;
-          sres[h][i] = res;
-        }
+        for (int mt = 0; mt < 4; ++mt) tot[mt] = tot[mt] + acc[mt];
+        ltot = ltot + lsum;
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          lsum = lsum + lins[h][i];
-          lprod = lprod * fac[h][i];
-        }
-        if (h == 1 && !two) break;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-            acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 * h + 4 * i + lq][16 * mt + lc], sres[h][i], acc[mt],
-                                                           0, 0, 0);
-      }
-      mmb_lg_renorm(&lprod, &lexp);  // < 2^9 before: never overflows
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = mmb_d4{0.0, 0.0, 0.0, 0.0};
+      lsum = 0.0;
+      lprod = 1.0;
+      lexp = 0;
     }
-    lsum = mmb_lg_lane_lp(lsum, lprod, lexp);
-    lsum = lsum + __shfl_xor(lsum, 16, 64);
-    lsum = lsum + __shfl_xor(lsum, 32, 64);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) tot[mt] = acc[mt];
-    ltot = lsum;
   }
   if (!live) return;
   // coefficient 16 mt + lq + 4 q of chain lc
-  double* gp = A.gpart + ((size_t)un * A.K + slot) * 64;
+  double* gp = A.gpart + ((size_t)un0 * A.K + slot) * 64;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) gp[16 * mt + lq + 4 * q] = tot[mt][q];
-  if (lq == 0) A.lpart[(size_t)un * A.K + slot] = ltot;
+    for (int qq = 0; qq < 4; ++qq) gp[16 * mt + lq + 4 * qq] = tot[mt][qq];
+  if (lq == 0) A.lpart[(size_t)un0 * A.K + slot] = ltot;
 }
 
 // nbound: an upper bound of the chains still running (the host's last read of the request
-// count; requests never increase within a window)
-hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, hipStream_t st) {
+// count; requests never increase within a window).  fold: the gradient kernel ran (or will run)
+// in group mode; the control kernel that consumes its partials gets the same flag.
+hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, int fold, hipStream_t st) {
   const dim3 grid(((start ? A.K : nbound) + 3) / 4), blk(256);
   if (A.kind == MMB_SAMPLER_HMC)
-    hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<false>>, grid, blk, 0, st, A, start, parity);
+    hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<false>>, grid, blk, 0, st, A, start, parity, fold);
   else if (A.kind == MMB_SAMPLER_MALA)
-    hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<true>>, grid, blk, 0, st, A, start, parity);
+    hipLaunchKernelGGL(lg_ctl_kernel<LgHmc<true>>, grid, blk, 0, st, A, start, parity, fold);
   else
-    hipLaunchKernelGGL(lg_ctl_kernel<LgNuts>, grid, blk, 0, st, A, start, parity);
+    hipLaunchKernelGGL(lg_ctl_kernel<LgNuts>, grid, blk, 0, st, A, start, parity, fold);
   return hipGetLastError();
 }
-hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, hipStream_t st) {
-  const dim3 grid(MMB_LG_NG * MMB_LG_NS * ((nbound + 63) / 64)), blk(256);
-  if (A.p <= 52)
-    hipLaunchKernelGGL(lg_grad_kernel<13>, grid, blk, 0, st, A, parity);
-  else
-    hipLaunchKernelGGL(lg_grad_kernel<16>, grid, blk, 0, st, A, parity);
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, int fold, hipStream_t st) {
+  const int tiles = (nbound + 63) / 64;
+  const dim3 grid((fold ? MMB_LG_NG : MMB_LG_NG * MMB_LG_NS) * tiles), blk(256);
+  if (A.p <= 52) {
+    if (fold) hipLaunchKernelGGL((lg_grad_kernel<13, true>), grid, blk, 0, st, A, parity);
+    else hipLaunchKernelGGL((lg_grad_kernel<13, false>), grid, blk, 0, st, A, parity);
+  } else {
+    if (fold) hipLaunchKernelGGL((lg_grad_kernel<16, true>), grid, blk, 0, st, A, parity);
+    else hipLaunchKernelGGL((lg_grad_kernel<16, false>), grid, blk, 0, st, A, parity);
+  }
   return hipGetLastError();
 }

@@ -391,6 +391,27 @@ def test_logistic_wide_parity(mamba, oracle, p):
         assert np.abs(dg[-1] - dg[0]).max() > 0
 
 
+def test_logistic_group_mode_parity(mamba, oracle):
+    """Wide gradient steps (>= MMB_LG_FOLD_MIN = 1024 running chains, engine.cpp) run one
+    workgroup per (group, tile) that forms the group's (P0 + P1) itself; narrower steps one
+    workgroup per sub-range.  NUTS with 1100 chains switches between the two as chains idle,
+    HMC with 1024 chains at N = 10000 (160-row sub-ranges) stays in group mode: bit-exact."""
+    m, _ = logistic(mamba, 1000, 50)
+    K = 1100
+    init = np.random.default_rng(31).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 6, 1, 1, model_burnin=3)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+    m, _ = logistic(mamba, 10000, 50, [mamba.HMC("beta", 0.005, 2)])
+    K = 1024
+    init = np.random.default_rng(32).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 2, 0, 1)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    assert eng.grad_evals() == 2 * K * 3
+
+
 def test_logistic_full_size_properties(mamba):
     """Config 4 at full size: N = 10000, p = 50, 4096 chains.  Finite draws, every update
     completed without hitting the depth cap, gradient count consistent with the tree
