@@ -998,11 +998,10 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
         HIPCHK(e, hipMemcpyAsync(e->lg_hcount + j, e->lg_count + (s & 1), sizeof(int32_t),
                                  hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipEventRecord(e->lg_cev[j], e->stream));
-        if (s >= 2 * LG_CHECK) {
-          HIPCHK(e, hipEventSynchronize(e->lg_cev[j ^ 1]));
-          if (e->lg_hcount[j ^ 1] == 0) break;
-          nbound = e->lg_hcount[j ^ 1];
-        }
+        const int jw = s >= 2 * LG_CHECK ? j ^ 1 : j;  // the first check waits for its own copy
+        HIPCHK(e, hipEventSynchronize(e->lg_cev[jw]));     // (short windows end without surplus)
+        if (e->lg_hcount[jw] == 0) break;
+        nbound = e->lg_hcount[jw];
       }
       if (s > cap) return fail(e, MMB_E_STATE, "logistic window did not terminate");
     }

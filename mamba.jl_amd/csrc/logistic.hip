@@ -221,7 +221,8 @@ __global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, 
   }
   if (S.pc == MC::IDLE) return;
   if (MC::wants(S.pc)) {
-    const int slot = A.iv[(size_t)c * MMB_LG_NIV + 10];
+    // the chain's gradient slot is its index in the request list (slot assignment below)
+    const int slot = start ? A.iv[(size_t)c * MMB_LG_NIV + 10] : si;
     if (fold) lg_assemble<true>(A, slot, lane, g, S);
     else lg_assemble<false>(A, slot, lane, g, S);
   }
