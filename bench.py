@@ -270,7 +270,11 @@ def main():
     mburn = pre + args.warmup if nuts else 0
     if pre > 0:
         eng.run(pre, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False)
-    eng.run(args.warmup, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False)
+    # warm-up with event timing on (the engine's event pools exist before the timed window),
+    # then the device draw buffer for the timed window's kept rows: no allocation in the window
+    eng.run(args.warmup, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False,
+            time_kernels=True)
+    eng.reserve_draws(args.steps // thin + 1)
     nuts_before = eng.nuts_stats() if nuts else None
     barrier()
     t0 = time.perf_counter()

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 4
+#define MMB_ABI_VERSION 5
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -239,6 +239,10 @@ int mmb_set_tune(mmb_engine* e, const double* tune);
 /* Draws of the last window kept on device (keep_device=1), host copy in Mamba order. */
 int64_t mmb_num_kept(const mmb_engine* e);
 int mmb_get_draws(mmb_engine* e, double* draws);
+/* Allocate the device draw buffer for windows keeping up to nkept iterations now, so a
+ * later mmb_run does not allocate inside a timed or latency-sensitive window (mmb_run grows
+ * the buffer itself when a window needs more).  nkept >= 0. */
+int mmb_reserve_draws(mmb_engine* e, int64_t nkept);
 
 /* Gelman-Rubin sufficient statistics of the device-kept draws (gelmandiag.jl:3-60).
  * mmb_gr_range: per monitored param [min, max] over local chains/draws (for link()).

@@ -75,6 +75,8 @@ set_tune!(e, t::Matrix{Float64}) = check(ccall((:mmb_set_tune, libmambahip), Cin
 set_iter!(e, it::Integer) = check(ccall((:mmb_set_iter, libmambahip), Cint, (Ptr{Void}, Int64), e, it), e)
 gr_len(e) = ccall((:mmb_gr_len, libmambahip), Int64, (Ptr{Void},), e)
 num_kept(e) = ccall((:mmb_num_kept, libmambahip), Int64, (Ptr{Void},), e)
+reserve_draws(e, nkept::Integer) =
+    check(ccall((:mmb_reserve_draws, libmambahip), Cint, (Ptr{Void}, Int64), e, nkept), e)
 
 # the one collective (mmb_comm_*): RCCL over xGMI inside the library
 function comm_id()

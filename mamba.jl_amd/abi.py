@@ -13,7 +13,7 @@ MMB_MAX_NODES_PER_BLOCK = 4
 MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC, MMB_MODEL_IR = 1, 2, 3, 4
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
-MMB_ABI_VERSION = 4
+MMB_ABI_VERSION = 5
 MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
 MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
@@ -101,6 +101,7 @@ def _declare(lib):
         "mmb_set_tune": (C.c_int, [P, D]),
         "mmb_num_kept": (I64, [P]),
         "mmb_get_draws": (C.c_int, [P, D]),
+        "mmb_reserve_draws": (C.c_int, [P, I64]),
         "mmb_gr_range": (C.c_int, [P, D]),
         "mmb_gr_len": (I64, [P]),
         "mmb_gr_partials": (C.c_int, [P, C.POINTER(I32), D, D]),

@@ -1120,6 +1120,23 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
   return 0;
 }
 
+int mmb_reserve_draws(mmb_engine* e, int64_t nkept) {
+  if (!e || nkept < 0) return fail(e, MMB_E_ARG, "null engine or nkept < 0");
+  if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  const size_t need = (size_t)nkept * e->pmon * e->K;
+  if (need > e->draws_cap) {
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // the old buffer may still be read by a kernel
+    if (e->d_draws) HIPCHK(e, hipFree(e->d_draws));
+    e->d_draws = nullptr;
+    e->draws_cap = 0;
+    e->n_kept = 0;  // the kept draws (if any) went with the old buffer
+    HIPCHK(e, dalloc(&e->d_draws, need));
+    e->draws_cap = need;
+  }
+  return 0;
+}
+
 int mmb_get_draws(mmb_engine* e, double* draws) {
   if (!e || !draws) return fail(e, MMB_E_ARG, "null argument");
   const int64_t nk = e->n_kept;

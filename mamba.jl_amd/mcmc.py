@@ -76,6 +76,11 @@ class Engine:
         self._chk(self.lib.mmb_run(self.h, C.byref(a)))
         return out
 
+    def reserve_draws(self, nkept):
+        """Allocate the device draw buffer for windows keeping up to `nkept` iterations now
+        (mmb_reserve_draws), so a later run does not allocate inside a timed window."""
+        self._chk(self.lib.mmb_reserve_draws(self.h, int(nkept)))
+
     @property
     def iter(self):
         return self.lib.mmb_iter(self.h)

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(mamba):
     assert len(syms) >= 20
     missing = [s for s in syms if s not in exported]
     assert not missing, missing
-    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 4
+    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 5
 
 
 def test_struct_layout_matches_header(mamba):
@@ -127,6 +127,7 @@ def test_comm_init_validates_before_touching_the_device(mamba):
     assert lib.mmb_comm_init(arr, 1, 1, 0, None, C.byref(h)) == -1          # null engine
     assert lib.mmb_range_allreduce(None, None) == -1
     assert lib.mmb_gr_allreduce(None, None, None, None) == -1
+    assert lib.mmb_reserve_draws(None, 8) == -1
     lib.mmb_comm_destroy(None)
 
 
