@@ -150,6 +150,23 @@ __device__ __forceinline__ double swap16_d(double x) {
   int lo = swap16_i((int)(uint32_t)u), hi = swap16_i((int)(uint32_t)(u >> 32));
   return mmb_u2d((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32));
 }
+// acc = fma(b, x of lane n of this lane's 16-lane row, acc): one v_fmac_f64 with a 64-bit DPP
+// row_newbcast source (gfx950 DPP64), i.e. a row broadcast without an LDS read per lane.  A source
+// lane disabled in EXEC would read as "no write", so callers keep every lane of the row active.
+template <int N>
+__device__ __forceinline__ void fmac_rowbc(double& acc, double x, double b) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc) : "v"(x), "v"(b), "n"(N));
+}
+__device__ __forceinline__ void fmac_rowbc_n(double& acc, double x, double b, int n) {
+  switch (n) {  // n is a constant after unrolling: one case survives
+#define MMB_RBC(i) case i: fmac_rowbc<i>(acc, x, b); break;
+    MMB_RBC(0) MMB_RBC(1) MMB_RBC(2) MMB_RBC(3) MMB_RBC(4) MMB_RBC(5) MMB_RBC(6) MMB_RBC(7)
+    MMB_RBC(8) MMB_RBC(9) MMB_RBC(10) MMB_RBC(11) MMB_RBC(12) MMB_RBC(13) MMB_RBC(14) MMB_RBC(15)
+#undef MMB_RBC
+  }
+}
+
 // stage s of the 32-lane all-reduce: partner lanes xor1, xor2 (quad_perm), 7-i (row_half_mirror),
 // 15-i (row_mirror), i^16 (permlane16_swap).  After stage s every lane of the 2^(s+1) subgroup
 // holds the same (commutative) combination.

@@ -403,8 +403,13 @@ struct Smp {
         // every lane forms sqrt / reciprocal of its own candidate before the search ends
         // (independent of it, so its latency overlaps the reductions); the pivot lane's pair
         // is the one used (out of the fast range: sqrt() and division on the pivot lane)
-        const double ajj_s = mmb_sqrt_inrange(dl);
-        const double rinv_s = mmb_rcp_inrange(ajj_s);
+        double ajj_s = mmb_sqrt_inrange(dl);
+        double rinv_s = mmb_rcp_inrange(ajj_s);
+#ifdef MMB_EXP_PIN_SQRT
+        // timing experiment: keep both sequences ahead of the search (the compiler otherwise
+        // sinks them into the pivot lane's branch); measured 1 % slower
+        asm volatile("" : "+v"(ajj_s), "+v"(rinv_s));
+#endif
         // key: high word of a positive candidate, INT_MAX for a NaN candidate, else -1
         // (three independent selects: no branchy nest for the compiler to serialise)
         const int hiw = (int)(mmb_d2u(dl) >> 32);
@@ -442,7 +447,28 @@ struct Smp {
           grp_sync();
           if (piv) { Lrow[j] = ajj; pe = j; }
           done = done || piv;
+#ifndef MMB_EXP_LDS_DOT
+          // pivot row: lane l of each 16-lane row reads elements l and 16 + l (two 8-byte reads
+          // instead of j/2 16-byte broadcast reads per lane), then every product takes element k
+          // from lane k % 16 of its row by a DPP64 row_newbcast operand.  Every lane of the group
+          // runs the dot product (a DPP source lane must be active); done lanes discard it.
+          double t0 = 0.0, t1 = 0.0;
+          // Sigma(lane, p) and the pivot's reciprocal are read with the row pieces (one LDS wait)
+          double sig = mat[mmb_slot(inb ? lane : 0, p)], rinv = prow[RI];
+          double pA = prow[lane & 15];
+          double pB = j > 16 ? prow[16 + (lane & 15)] : 0.0;
+          asm volatile("" : "+v"(sig), "+v"(rinv), "+v"(pA), "+v"(pB));
+          if (j > 0) {
+#pragma unroll
+            for (int k = 0; k < j; ++k) {
+              const double src = k < 16 ? pA : pB;
+              if (k & 1) fmac_rowbc_n(t1, src, Lrow[k], k & 15);
+              else fmac_rowbc_n(t0, src, Lrow[k], k & 15);
+            }
+          }
+#endif
           if (!done) {
+#ifdef MMB_EXP_LDS_DOT
             double t0 = 0.0, t1 = 0.0;
 #pragma unroll
             for (int k = 0; k + 1 < j; k += 2) {
@@ -451,7 +477,9 @@ struct Smp {
               t1 = fma(Lrow[k + 1], pp.y, t1);
             }
             if (j & 1) t0 = fma(Lrow[j - 1], prow[j - 1], t0);
-            const double lij = (mat[mmb_slot(lane, p)] - (t0 + t1)) * prow[RI];
+            const double sig = mat[mmb_slot(lane, p)], rinv = prow[RI];
+#endif
+            const double lij = (sig - (t0 + t1)) * rinv;
             Lrow[j] = lij;
             work = work + lij * lij;
           }
