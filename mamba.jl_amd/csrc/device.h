@@ -36,6 +36,28 @@ __device__ __forceinline__ double mmb_sqrt_inrange(double x) {
   d = fma(-g, g, x);
   return fma(d, h, g);
 }
+// Both at once for the pivoted Cholesky: s = sqrt(x) as mmb_sqrt_inrange, r = 1.0 / s as
+// mmb_rcp_inrange(s), but the reciprocal starts from the Goldschmidt half-reciprocal h
+// (2h ~ 1/sqrt(x) to about the square of the rsq error) instead of a second transcendental:
+// one Newton step and the same final correction fma(e, r, r).  Checked bit for bit against
+// sqrt() and 1.0 / sqrt() over the whole fast range by tools/sqrt_rcp_check.hip.
+__device__ __forceinline__ void mmb_sqrt_rcp_inrange(double x, double* s, double* rcp) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  double q = h + h;
+  double e = fma(-g, q, 1.0);
+  q = fma(q, e, q);
+  e = fma(-g, q, 1.0);
+  *rcp = fma(e, q, q);
+  *s = g;
+}
 __device__ __forceinline__ double mmb_rcp_inrange(double y) {
   double r = __builtin_amdgcn_rcp(y);
   double e = fma(-y, r, 1.0);

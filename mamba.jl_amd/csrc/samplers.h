@@ -403,8 +403,13 @@ struct Smp {
         // every lane forms sqrt / reciprocal of its own candidate before the search ends
         // (independent of it, so its latency overlaps the reductions); the pivot lane's pair
         // is the one used (out of the fast range: sqrt() and division on the pivot lane)
+#ifdef MMB_EXP_RCP_SEQ
         double ajj_s = mmb_sqrt_inrange(dl);
         double rinv_s = mmb_rcp_inrange(ajj_s);
+#else
+        double ajj_s, rinv_s;
+        mmb_sqrt_rcp_inrange(dl, &ajj_s, &rinv_s);
+#endif
 #ifdef MMB_EXP_PIN_SQRT
         // timing experiment: keep both sequences ahead of the search (the compiler otherwise
         // sinks them into the pivot lane's branch); measured 1 % slower
