@@ -175,14 +175,22 @@ __device__ __forceinline__ double swap16_d(double x) {
 // acc = fma(b, x of lane n of this lane's 16-lane row, acc): one v_fmac_f64 with a 64-bit DPP
 // row_newbcast source (gfx950 DPP64), i.e. a row broadcast without an LDS read per lane.  A source
 // lane disabled in EXEC would read as "no write", so callers keep every lane of the row active.
-template <int N>
+// The compiler's hazard recognizer does not look inside inline asm, so the first use of a
+// source value (first = true) starts with the two wait states a DPP read needs after a VALU
+// write of its source; later uses of the same value follow DPP instructions only.
+template <int N, bool FIRST>
 __device__ __forceinline__ void fmac_rowbc(double& acc, double x, double b) {
-  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-               : "+v"(acc) : "v"(x), "v"(b), "n"(N));
+  if constexpr (FIRST)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(x), "v"(b), "n"(N));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(x), "v"(b), "n"(N));
 }
+// n = k % 16 of a dot product over k ascending: the uses at k = 0 and k = 16 are first uses
 __device__ __forceinline__ void fmac_rowbc_n(double& acc, double x, double b, int n) {
   switch (n) {  // n is a constant after unrolling: one case survives
-#define MMB_RBC(i) case i: fmac_rowbc<i>(acc, x, b); break;
+#define MMB_RBC(i) case i: fmac_rowbc<i, i == 0>(acc, x, b); break;
     MMB_RBC(0) MMB_RBC(1) MMB_RBC(2) MMB_RBC(3) MMB_RBC(4) MMB_RBC(5) MMB_RBC(6) MMB_RBC(7)
     MMB_RBC(8) MMB_RBC(9) MMB_RBC(10) MMB_RBC(11) MMB_RBC(12) MMB_RBC(13) MMB_RBC(14) MMB_RBC(15)
 #undef MMB_RBC

@@ -502,10 +502,11 @@ struct Smp {
       double a = 0.0;
       if (inb) a = fma(NB->sigl[lane * d + lane], z1n, a);
       if (m > 2 * d) {
-        prow[lane] = z2n;
-        grp_sync();
         // rows are zero past the lane's own step, so the full sweep adds exact zeros
         double y = 0.0;
+#ifdef MMB_EXP_LDS_CARRY
+        prow[lane] = z2n;
+        grp_sync();
 #pragma unroll
         for (int k = 0; k < DMAX; k += 2) {
           const double2 zz = *(const double2*)(prow + k);
@@ -513,6 +514,15 @@ struct Smp {
           if (k + 1 < DMAX) y = fma(Lrow[k + 1], zz.y, y);
         }
         grp_sync();
+#else
+        // z2'[k] lives in lane k: rows 0 / 1 of the group exchange theirs (permlane16 swap),
+        // then each product takes z2'[k] from lane k % 16 of the row (DPP64 row_newbcast)
+        const double zs = swap16_d(z2n);
+        const bool row0 = (lane & 16) == 0;
+        const double zA = row0 ? z2n : zs, zB = row0 ? zs : z2n;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) fmac_rowbc_n(y, k < 16 ? zA : zB, Lrow[k], k & 15);
+#endif
         a = NB->beta * a + (1.0 - NB->beta) * y;
       }
       if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
