@@ -768,28 +768,40 @@ struct Smp {
       double lt[NT];
 #pragma unroll
       for (int u = 0; u < NT; ++u) lt[u] = (!fresh && u * G + g.lane < T) ? Mvv[u * G + g.lane] : 0.0;
+      // slot t = u G + lane: HBM and LDS addresses are the lane's base + a constant per u
+      // (immediate offsets), the fresh / steady choice is made once outside the slot loop
+      double* const Mvv_l = Mvv + g.lane;
+      double* const mat_l = mat + g.lane;
+      auto slots = [&](auto fresh_c) {
+        constexpr bool FRESH = decltype(fresh_c)::value;
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        int t = u * G + g.lane;
-        // opaque to the optimiser: recomputing (i, k) here is a few VALU ops, while
-        // hoisting all NT pairs out of the iteration loop keeps 2*NT ints live (spills)
-        asm volatile("" : "+v"(t));
-        if (t < T) {
-          int i, k;
-          if constexpr (IKTAB) {
-            const int w = ik_table()[t];
-            i = w >> 8;
-            k = w & 255;
-          } else {
-            slot_ik(t, i, k);
+        for (int u = 0; u < NT; ++u) {
+          const int t = u * G + g.lane;
+          if (t < T) {
+            // opaque to the optimiser: decoding (i, k) here is a few VALU ops, while hoisting
+            // all NT pairs out of the iteration loop keeps 2*NT ints live (spills)
+            int i, k;
+            if constexpr (IKTAB) {
+              int li = g.lane;
+              asm volatile("" : "+v"(li));
+              const int w = ik_table()[li + u * G];
+              i = w >> 8;
+              k = w & 255;
+            } else {
+              int ti = t;
+              asm volatile("" : "+v"(ti));
+              slot_ik(ti, i, k);
+            }
+            const double2 a = vm[k], bi = vm[i];
+            const double old = FRESH ? z2s[i] * z2s[k] : lt[u];
+            const double nv = p * old + (q * a.x) * bi.x;
+            Mvv_l[u * G] = nv;
+            mat_l[u * G] = cc * (nv - a.y * bi.y);
           }
-          const double2 a = vm[k], bi = vm[i];
-          double old = fresh ? z2s[i] * z2s[k] : lt[u];
-          double nv = p * old + (q * a.x) * bi.x;
-          Mvv[t] = nv;
-          mat[t] = cc * (nv - a.y * bi.y);
         }
-      }
+      };
+      if (fresh) slots(std::true_type{});
+      else slots(std::false_type{});
       grp_sync();
       // everything but the factorization is finished first; the chain state is parked
       // in LDS so the Cholesky's register footprint does not stack on top of it
