@@ -438,9 +438,11 @@ struct Smp {
           const bool piv = lane == p;
           double ajj = 0.0;
           if (piv) {
+            if (j + 1 < d) {  // the last step has no rows left to update: no readers
 #pragma unroll
-            for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
-            if (j & 1) prow[j - 1] = Lrow[j - 1];
+              for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
+              if (j & 1) prow[j - 1] = Lrow[j - 1];
+            }
             ajj = ajj_s;  // IEEE results in the fast range (device.h)
             double rinv = rinv_s;
             if (!mmb_fast_range(dl)) {
@@ -463,7 +465,7 @@ struct Smp {
           double pA = prow[lane & 15];
           double pB = j > 16 ? prow[16 + (lane & 15)] : 0.0;
           asm volatile("" : "+v"(sig), "+v"(rinv), "+v"(pA), "+v"(pB));
-          if (j > 0) {
+          if (j > 0 && j + 1 < d) {  // (j = d - 1: every lane is done)
 #pragma unroll
             for (int k = 0; k < j; ++k) {
               const double src = k < 16 ? pA : pB;
