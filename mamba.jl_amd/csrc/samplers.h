@@ -400,9 +400,8 @@ struct Smp {
     for (int j = 0; j < DMAX; ++j) {
       if (live && j < d) {
         const double dl = diag0 - work;
-        // every lane forms sqrt / reciprocal of its own candidate before the search ends
-        // (independent of it, so its latency overlaps the reductions); the pivot lane's pair
-        // is the one used (out of the fast range: sqrt() and division on the pivot lane)
+        // sqrt / reciprocal of the candidate (the compiler keeps them on the pivot lane's
+        // path); out of the fast range the pivot lane takes sqrt() and division instead
 #ifdef MMB_EXP_RCP_SEQ
         double ajj_s = mmb_sqrt_inrange(dl);
         double rinv_s = mmb_rcp_inrange(ajj_s);
