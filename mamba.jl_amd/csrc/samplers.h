@@ -386,6 +386,7 @@ struct Smp {
     const int lane = g.lane;
     const bool hi_half = (threadIdx.x & 32) != 0;
     const bool inb = lane < d;
+    const int lc = inb ? lane : 0;
     const double diag0 = inb ? mat[mmb_tri(lane) + lane] : 0.0;
     double work = 0.0;
     double Lrow[DMAX];
@@ -460,7 +461,13 @@ struct Smp {
           // runs the dot product (a DPP source lane must be active); done lanes discard it.
           double t0 = 0.0, t1 = 0.0;
           // Sigma(lane, p) and the pivot's reciprocal are read with the row pieces (one LDS wait)
-          double sig = mat[mmb_slot(inb ? lane : 0, p)], rinv = prow[RI];
+          // Sigma(lc, p) at byte 8 slot = 4 a (a + 1) + 8 b, a = max, b = min: max, min, one
+          // 24-bit multiply-add and two shift-adds
+          const int sa = max(lc, p), sb = min(lc, p);
+          int sq;  // sa (sa + 1) in one instruction (the compiler splits it into three)
+          asm("v_mad_u32_u24 %0, %1, %1, %1" : "=v"(sq) : "v"(sa));
+          double sig = *(const double*)((const char*)mat + ((sq + 2 * sb) << 2));
+          double rinv = prow[RI];
           double pA = prow[lane & 15];
           double pB = j > 16 ? prow[16 + (lane & 15)] : 0.0;
           asm volatile("" : "+v"(sig), "+v"(rinv), "+v"(pA), "+v"(pB));
