@@ -13,6 +13,7 @@
 module MambaHIP
 
 using Mamba
+import Distributions: Univariate, Multivariate
 import Mamba: Model, Sampler, ModelState, ModelChains, Chains, AMWGTune, AMMTune, NUTSTune,
               SliceTune, HMCTune, MALATune, SamplerTune, relist!, unlist, gettune
 
@@ -102,6 +103,64 @@ function gr_allreduce(c, e, link::Vector{Int32}, shift::Vector{Float64})
               c, link, shift, out), e); out
 end
 
+# ---- sampler registry ------------------------------------------------------------------------
+# `Sampler(params, samplerfx, tune)` stores `modelfx(samplerfxargs, samplerfx)` in `s.eval`
+# (src/samplers/sampler.jl:22-24): a new top-level function `eval`'d from an AST
+# (src/utils.jl:3-12) whose body names the closure as a literal.  It has no fields, so a
+# sampler's constructor arguments (sigma, Sigma, width, form, pargs, adapt, keyword args)
+# cannot be read back from the Sampler.  The MambaHIP constructors below call Mamba's own and
+# record those arguments here, keyed by the `s.eval` object: `mcmc` deep-copies the Model
+# (src/model/mcmc.jl:27), which copies every Sampler but returns a field-less object itself
+# (Base deepcopy_internal: `nfields(T) == 0 && return x`), so the key survives the copy.
+# `lower` reads only this registry; an unregistered block keeps the Julia path.
+immutable HIPSampler
+  kind::Int32
+  pargs::Tuple                     # positional constructor arguments after `params`
+  kwargs::Dict{Symbol,Any}         # keyword arguments, incl. `adapt` with its default
+end
+const REGISTRY = ObjectIdDict()
+
+function register(s::Sampler, kind::Int32, pargs::Tuple, kwargs)
+  d = Dict{Symbol,Any}()
+  for (k, v) in kwargs; d[k] = v; end
+  REGISTRY[s.eval] = HIPSampler(kind, pargs, d)
+  s
+end
+registered(s::Sampler) = get(REGISTRY, s.eval, nothing)
+kwarg(r::HIPSampler, name::Symbol, default) = get(r.kwargs, name, default)
+
+"A Gibbs block the engine runs natively: `Sampler(params, f, GibbsTune())` with f the
+conjugate full conditional of INTEGRATION.md §3 (the Julia path still calls f)."
+type GibbsTune <: SamplerTune end
+Gibbs(params::Vector{Symbol}, f::Function) =
+  register(Sampler(params, f, GibbsTune()), MMB_SAMPLER_GIBBS, (), ())
+
+# Same signatures and defaults as the reference constructors; each returns Mamba's Sampler.
+AMWG(params, sigma; adapt::Symbol=:all, args...) =                           # amwg.jl:47-61
+  register(Mamba.AMWG(params, sigma; adapt=adapt, args...), MMB_SAMPLER_AMWG, (sigma,),
+           Any[(:adapt, adapt), args...])
+AMM(params, Sigma::Matrix; adapt::Symbol=:all, args...) =                    # amm.jl:45-59
+  register(Mamba.AMM(params, Sigma; adapt=adapt, args...), MMB_SAMPLER_AMM, (Sigma,),
+           Any[(:adapt, adapt), args...])
+NUTS(params; dtype::Symbol=:forward, args...) =                              # nuts.jl:47-56
+  register(Mamba.NUTS(params; dtype=dtype, args...), MMB_SAMPLER_NUTS, (),
+           Any[(:dtype, dtype), args...])
+Slice(params, width, F::Type=Multivariate; transform::Bool=false) =          # slice.jl:47-58
+  register(Mamba.Slice(params, width, F; transform=transform), MMB_SAMPLER_SLICE, (width, F),
+           Any[(:transform, transform)])
+HMC(params, epsilon::Real, L::Integer, pargs...; dtype::Symbol=:forward) =   # hmc.jl:47-65
+  register(Mamba.HMC(params, epsilon, L, pargs...; dtype=dtype), MMB_SAMPLER_HMC, (epsilon, L, pargs...),
+           Any[(:dtype, dtype)])
+MALA(params, epsilon::Real, pargs...; dtype::Symbol=:forward) =              # mala.jl:43-58
+  register(Mamba.MALA(params, epsilon, pargs...; dtype=dtype), MMB_SAMPLER_MALA, (epsilon, pargs...),
+           Any[(:dtype, dtype)])
+
+# tune type each constructor creates (amwg.jl:60, amm.jl:58, nuts.jl:55, slice.jl:57,
+# hmc.jl:64, mala.jl:59): a registered block must still carry it
+const TUNE_OF = Dict(MMB_SAMPLER_AMWG => AMWGTune, MMB_SAMPLER_AMM => AMMTune, MMB_SAMPLER_NUTS => NUTSTune,
+                     MMB_SAMPLER_SLICE => SliceTune, MMB_SAMPLER_HMC => HMCTune, MMB_SAMPLER_MALA => MALATune,
+                     MMB_SAMPLER_GIBBS => GibbsTune)
+
 # ---- model lowering --------------------------------------------------------------------------
 # Engine value layout per model kind (include/mamba_hip.h node ids; model.py offsets):
 const LAYOUT = Dict(
@@ -110,33 +169,57 @@ const LAYOUT = Dict(
                      (:beta, 4, 30), (:mu_beta, 5, 1), (:s2_beta, 6, 1)],  # doc/examples/rats.jl:48-97
   MMB_MODEL_LOGISTIC => [(:beta, 0, 0)])                                   # SURVEY §8a, p from the node
 
-"A Gibbs block the engine runs natively: `Sampler(params, f, GibbsTune())` with f the
-conjugate full conditional of INTEGRATION.md §3 (the Julia path still calls f)."
-type GibbsTune <: SamplerTune end
-Gibbs(params::Vector{Symbol}, f::Function) = Sampler(params, f, GibbsTune())
-
 function model_kind(m::Model)
   ks = Set(keys(m, :dependent))                     # Logical + Stochastic nodes (inputs excluded)
   ks == Set([:y, :beta, :s2, :mu]) && return MMB_MODEL_LINE
   ks == Set([:y, :alpha, :alpha0, :mu_alpha, :s2_alpha, :beta, :mu_beta, :s2_beta, :s2_c]) &&
     return MMB_MODEL_RATS
   ks == Set([:y, :p, :beta]) && return MMB_MODEL_LOGISTIC
-  nothing                                           # (node IR lowering: INTEGRATION.md §2a)
+  nothing                                           # any other DAG: lower_ir (below)
 end
 
 node_id(kind, key::Symbol) = (for (k, id, _) in LAYOUT[kind]; k == key && return id; end; nothing)
-captured(f::Function, name::Symbol, default) = name in fieldnames(typeof(f)) ? getfield(f, name) : default
-function kwarg(f::Function, name::Symbol, default)
-  for (k, v) in captured(f, :args, [])           # AMM(...; beta=, scale=) keyword splat
-    k == name && return v
+fillvec(x, n) = isa(x, Real) ? fill(Float64(x), n) : Float64[x...]
+
+"Sampler b -> BlockSpec (+ buffers to keep alive), or nothing when the block is not registered.
+Argument errors are the reference's own (amwg.jl:37-42, amm.jl:35-40, slice.jl:36-43, hmc.jl:38-44)."
+function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::Integer, keep::Vector{Any})
+  r = registered(s)
+  r === nothing && return nothing                   # an arbitrary user closure: keep the Julia path
+  isa(s.tune, TUNE_OF[r.kind]) || return nothing
+  blk(adapt_, form, transform, batchsize, target, beta, scale, tun, eps, L) =
+    BlockSpec(r.kind, nnodes, nodes, adapt_, form, transform, batchsize, target, beta, scale, dim,
+              length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L, 0)
+  adapt = MMB_ADAPT[kwarg(r, :adapt, :none)]
+  if r.kind == MMB_SAMPLER_GIBBS
+    return blk(MMB_ADAPT[:none], 0, 0, 0, 0.0, 0.0, 0.0, Float64[], 0.0, 0)
+  elseif r.kind == MMB_SAMPLER_AMWG                                            # amwg.jl:5-33
+    sig = fillvec(r.pargs[1], dim); push!(keep, sig)
+    length(sig) == dim || throw(ArgumentError("length(sigma) differs from variate length $dim"))
+    return blk(adapt, 0, 1, kwarg(r, :batchsize, 50), kwarg(r, :target, 0.44), 0.0, 0.0, sig, 0.0, 0)
+  elseif r.kind == MMB_SAMPLER_AMM                                             # amm.jl:5-30
+    Sig = vec(Float64[r.pargs[1]...]); push!(keep, Sig)                         # column-major
+    size(r.pargs[1], 1) == dim || throw(ArgumentError("Sigma dimension differs from variate length $dim"))
+    return blk(adapt, 0, 1, 0, 0.0, kwarg(r, :beta, 0.05), kwarg(r, :scale, 2.38), Sig, 0.0, 0)
+  elseif r.kind == MMB_SAMPLER_NUTS                                            # nuts.jl:5-39
+    return blk(MMB_ADAPT[:burnin], 0, 1, 0, kwarg(r, :target, 0.6), 0.0, 0.0, Float64[], 0.0, 0)
+  elseif r.kind == MMB_SAMPLER_SLICE                                           # slice.jl:7-26
+    w = fillvec(r.pargs[1], dim); push!(keep, w)
+    length(w) == dim || throw(ArgumentError("length(width) differs from variate length $dim"))
+    form = r.pargs[2] == Univariate ? Int32(1) : Int32(0)
+    return blk(MMB_ADAPT[:none], form, Int32(kwarg(r, :transform, false)), 0, 0.0, 0.0, 0.0, w, 0.0, 0)
+  else                                                                         # hmc.jl:5-32, mala.jl:5-30
+    hmc = r.kind == MMB_SAMPLER_HMC
+    nS = hmc ? 3 : 2                                  # (epsilon, L[, Sigma]) / (epsilon[, Sigma])
+    S = length(r.pargs) >= nS ? vec(Float64[r.pargs[nS]...]) : Float64[]; push!(keep, S)
+    isempty(S) || size(r.pargs[nS], 1) == dim ||
+      throw(ArgumentError("Sigma dimension differs from variate length $dim"))
+    return blk(MMB_ADAPT[:none], 0, 1, 0, 0.0, 0.0, 0.0, S, Float64(r.pargs[1]),
+               hmc ? Int32(r.pargs[2]) : Int32(0))
   end
-  default
 end
 
-"Model -> (ModelSpec, buffers to keep alive) or nothing (Julia path).  Mirror: model.py Model.spec().
-The sampler kind comes from the type of `s.tune` (created by each constructor, amwg.jl:60,
-amm.jl:58, nuts.jl:55, slice.jl:57, hmc.jl:64, mala.jl:59); constructor arguments are the
-variables the `samplerfx` closure captured (sigma / Sigma / width / pargs / adapt / args)."
+"Model -> (ModelSpec, buffers to keep alive) or nothing (Julia path).  Mirror: model.py Model.spec()."
 function lower(m::Model)
   kind = model_kind(m)
   kind === nothing && return nothing
@@ -153,37 +236,8 @@ function lower(m::Model)
     end
     nodes = ntuple(i -> i <= length(ids) ? ids[i] : Int32(0), 4)
     dim = sum(p -> length(m[p].value), s.params)
-    t, f = s.tune, s.eval
-    adapt = MMB_ADAPT[captured(f, :adapt, :none)]
-    blk(kind_, adapt_, form, transform, batchsize, target, beta, scale, tun, eps, L) =
-      BlockSpec(kind_, length(ids), nodes, adapt_, form, transform, batchsize, target, beta, scale, dim,
-                length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L, 0)
-    if isa(t, GibbsTune)
-      sp = blk(MMB_SAMPLER_GIBBS, MMB_ADAPT[:none], 0, 0, 0, 0.0, 0.0, 0.0, Float64[], 0.0, 0)
-    elseif isa(t, AMWGTune)                                                    # amwg.jl:47-61
-      sig = Float64[captured(f, :sigma, 1.0)...]; push!(keep, sig)
-      sp = blk(MMB_SAMPLER_AMWG, adapt, 0, 1, kwarg(f, :batchsize, 50), kwarg(f, :target, 0.44), 0.0, 0.0,
-               sig, 0.0, 0)
-    elseif isa(t, AMMTune)                                                     # amm.jl:45-59
-      Sig = vec(Float64[captured(f, :Sigma, eye(dim))...]); push!(keep, Sig)   # column-major
-      sp = blk(MMB_SAMPLER_AMM, adapt, 0, 1, 0, 0.0, kwarg(f, :beta, 0.05), kwarg(f, :scale, 2.38), Sig, 0.0, 0)
-    elseif isa(t, NUTSTune)                                                    # nuts.jl:47-56
-      sp = blk(MMB_SAMPLER_NUTS, MMB_ADAPT[:burnin], 0, 1, 0, kwarg(f, :target, 0.6), 0.0, 0.0, Float64[], 0.0, 0)
-    elseif isa(t, SliceTune)                                                   # slice.jl:47-58
-      w = Float64[captured(f, :width, 1.0)...]; push!(keep, w)
-      form = isa(t, SliceTune{Univariate}) ? Int32(1) : Int32(0)
-      sp = blk(MMB_SAMPLER_SLICE, MMB_ADAPT[:none], form, Int32(captured(f, :transform, false)), 0, 0.0, 0.0,
-               0.0, w, 0.0, 0)
-    elseif isa(t, HMCTune) || isa(t, MALATune)                                 # hmc.jl:47-65, mala.jl:43-58
-      pargs = captured(f, :pargs, ())                  # (epsilon, L[, Sigma]) / (epsilon[, Sigma])
-      hmc = isa(t, HMCTune)
-      nS = hmc ? 3 : 2
-      S = length(pargs) >= nS ? vec(Float64[pargs[nS]...]) : Float64[]; push!(keep, S)
-      sp = blk(hmc ? MMB_SAMPLER_HMC : MMB_SAMPLER_MALA, MMB_ADAPT[:none], 0, 1, 0, 0.0, 0.0, 0.0, S,
-               Float64(pargs[1]), hmc ? Int32(pargs[2]) : Int32(0))
-    else
-      return nothing                                # an arbitrary user closure: keep the Julia path
-    end
+    sp = block_spec(s, nodes, length(ids), dim, keep)
+    sp === nothing && return nothing
     blocks[b] = sp
   end
   nobs = kind == MMB_MODEL_LOGISTIC ? length(m[:y].value) : 0
@@ -338,6 +392,7 @@ function run_chains!(m::Model, window::UnitRange{Int}, burnin::Integer, thin::In
   try
     for (name, x) in inputs(m, kind); set_data!(e, name, x); end
     states = m.states
+    length(states) == length(chains) || throw(ArgumentError("one ModelState per chain expected"))
     init = hcat([(relist!(m, st.value); engine_values(m, kind)) for st in states]...)   # P x K
     offset = first(chains) - 1
     chains == offset + (1:length(chains)) || throw(ArgumentError("chains must be a contiguous range"))
@@ -345,11 +400,18 @@ function run_chains!(m::Model, window::UnitRange{Int}, burnin::Integer, thin::In
     first(window) > 1 && set_tune!(e, pack_tunes(m, states, first(window) - 1))        # restart
     set_iter!(e, first(window) - 1)
     K = length(chains)
-    nkept = length(filter(i -> i > burnin && (i - burnin) % thin == 0, window))
-    names = Mamba.names(m, true)
-    sim = Chains(nkept, length(names), chains=K, start=first(filter(i -> i > burnin && (i - burnin) % thin == 0,
-                                                                     window)), thin=thin, names=names)
-    a = RunArgs(length(window), burnin, thin, m.burnin, pointer(sim.value), 0, 0)
+    # draws are sized exactly as mcmc_worker! sizes them (src/model/mcmc.jl:70-71):
+    # Chains(last(window), p, start=burnin+thin, thin=thin) has length(burnin+thin:thin:last(window))
+    # rows (src/output/chains.jl:5-11), and the keep rule of mcmc.jl:76 fills row
+    # (i - burnin) / thin for every kept i of the window.  mmb_run writes n_kept rows.
+    nkept = count(i -> i > burnin && (i - burnin) % thin == 0, window)
+    pnames = Mamba.names(m, true)
+    sim = Chains(last(window), length(pnames), start=burnin + thin, thin=thin, chains=K, names=pnames)
+    size(sim.value, 1) == nkept ||
+      throw(ArgumentError("window $window, burnin $burnin, thin $thin: $(size(sim.value, 1)) Chains rows " *
+                          "but $nkept kept iterations"))
+    size(sim.value, 2) == num_monitored(e) || return nothing   # monitor flags the engine does not lower
+    a = RunArgs(length(window), burnin, thin, m.burnin, nkept == 0 ? Ptr{Float64}(C_NULL) : pointer(sim.value), 0, 0)
     run!(e, a)                                         # writes n x p x K in Chains order
     store_states!(m, e, kind, states)
     m.iter = last(window)

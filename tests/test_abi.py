@@ -141,3 +141,64 @@ def test_julia_shim_binds_declared_symbols():
     need = {"mmb_create", "mmb_set_data", "mmb_init_chains", "mmb_run", "mmb_get_values", "mmb_get_tune",
             "mmb_set_tune", "mmb_set_iter", "mmb_comm_init", "mmb_gr_allreduce", "mmb_range_allreduce"}
     assert need <= bound, need - bound
+
+
+def _julia_src():
+    return open(os.path.join(ROOT, "julia", "MambaHIP.jl")).read()
+
+
+def test_julia_shim_reads_sampler_args_from_the_registry():
+    """`s.eval` is modelfx's eval'd wrapper (src/samplers/sampler.jl:22-24, src/utils.jl:3-12):
+    it has no fields, so the shim must not try to read constructor arguments from it.  Every
+    sampler constructor the engine lowers is wrapped and registers its arguments."""
+    src = _julia_src()
+    code = "\n".join(l.split("#")[0] for l in src.splitlines())  # comments may name s.eval
+    assert not re.search(r"\b(getfield|fieldnames)\s*\(", code), "no reflection on closures"
+    assert not re.search(r"captured\s*\(", code)
+    uses = re.findall(r"s\.eval\b", code)
+    assert uses and all(u == "s.eval" for u in uses)
+    # s.eval is used only as the registry key
+    for line in code.splitlines():
+        if "s.eval" in line:
+            assert "REGISTRY" in line, line
+    for ctor in ["AMWG", "AMM", "NUTS", "Slice", "HMC", "MALA"]:
+        assert re.search(rf"^{ctor}\(params.*=\s*$", code, re.M), ctor
+        assert f"register(Mamba.{ctor}(params" in code, ctor
+    assert "register(Sampler(params, f, GibbsTune())" in code
+    # lower goes through block_spec, which returns nothing for an unregistered sampler
+    blk = code[code.index("function block_spec"):code.index("function lower(")]
+    assert "r === nothing && return nothing" in blk
+
+
+def test_julia_shim_sizes_draws_like_mcmc_worker():
+    """mcmc_worker! allocates Chains(last(window), p, start=burnin+thin, thin=thin)
+    (src/model/mcmc.jl:70-71) = length(burnin+thin:thin:last(window)) rows
+    (src/output/chains.jl:5-11); the shim must allocate the same and check it equals the
+    engine's kept count before handing the pointer to mmb_run."""
+    code = _julia_src()
+    rc = code[code.index("function run_chains!"):]
+    rc = rc[:rc.index("\nend\n")]
+    assert re.search(r"Chains\(last\(window\), length\(pnames\), start=burnin \+ thin, thin=thin", rc)
+    assert "size(sim.value, 1) == nkept" in rc
+    assert "Ptr{Float64}(C_NULL)" in rc          # a window that keeps nothing: no pointer into []
+    assert "first(filter" not in rc
+
+
+def test_julia_chains_rows_equal_kept_count():
+    """The invariant the shim's guard checks, over windows mcmc() and mcmc(mc, iters) produce:
+    first run 1:iters, and a restart whose burnin is last(mc) with last(mc) the last kept
+    iteration (mcmc.jl:3-16: last(mc) == div(iter, thin) * thin)."""
+    cases = []
+    for iters in (1, 7, 60, 1000):
+        for burnin in (0, 3, 250):
+            for thin in (1, 2, 3, 7):
+                if iters > burnin:
+                    cases.append((1, iters, burnin, thin))
+    for it0 in (10, 11, 1000, 1001):
+        for thin in (1, 2, 3):
+            last_kept = (it0 // thin) * thin
+            cases.append((it0 + 1, it0 + 37, last_kept, thin))
+    for first, last, burnin, thin in cases:
+        rows = len(range(burnin + thin, last + 1, thin))
+        kept = sum(1 for i in range(first, last + 1) if i > burnin and (i - burnin) % thin == 0)
+        assert rows == kept, (first, last, burnin, thin)
