@@ -1253,11 +1253,31 @@ int mmb_get_tune(mmb_engine* e, double* tune) {
 int mmb_set_tune(mmb_engine* e, const double* tune) {
   if (!e || !tune) return fail(e, MMB_E_ARG, "null argument");
   if (!e->d_vals) return fail(e, MMB_E_STATE, "mmb_init_chains not called");
+  const int64_t TL = mmb_tune_len(e), K = e->K;
+  const size_t DP = e->DP, TP = e->TP;
+  // validate every row before any device state changes: a valid AMM factor (t[2] != 0) needs
+  // its pivot order to be a permutation of 0..d-1 (it indexes the caller's row and the device
+  // factor); an invalid one is stored with identity positions whatever its pivot bytes hold
+  for (int64_t off = 0, b = 0; b < (int64_t)e->blocks.size(); off += e->blocks[b].tune_len, ++b) {
+    const auto& h = e->blocks[b];
+    if (h.spec.sampler != MMB_SAMPLER_AMM) continue;
+    for (int64_t k = 0; k < K; ++k) {
+      const double* t = tune + k * TL + off;
+      if (t[2] == 0.0) continue;
+      const double* pv = t + 4 + h.d + 2 * h.T;
+      uint32_t seen = 0;
+      for (int i = 0; i < h.d; ++i) {
+        const double v = pv[i];
+        if (!(v >= 0.0 && v < h.d) || v != (double)(int)v || (seen >> (int)v & 1u))
+          return fail(e, MMB_E_ARG, "block %d chain %lld: AMM pivot order is not a permutation of 0..%d",
+                      (int)b + 1, (long long)k, h.d - 1);
+        seen |= 1u << (int)v;
+      }
+    }
+  }
   ++e->xepoch;
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  const int64_t TL = mmb_tune_len(e), K = e->K;
-  const size_t DP = e->DP, TP = e->TP;
   int64_t off = 0;
   for (auto& h : e->blocks) {
     std::vector<int32_t> m(K, 0), fl(K, 0);
@@ -1283,14 +1303,15 @@ int mmb_set_tune(mmb_engine* e, const double* tune) {
         p += h.d;
         for (int s = 0; s < h.T; ++s) mvv[k * TP + s] = p[s];
         p += h.T;
+        const bool valid = t[2] != 0.0;
         if (amm_posform(e)) {
           std::vector<uint8_t> piv(h.d);
-          for (int i = 0; i < h.d; ++i) piv[i] = (uint8_t)p[h.T + i];
+          for (int i = 0; i < h.d; ++i) piv[i] = valid ? (uint8_t)p[h.T + i] : (uint8_t)i;
           slot_to_pos(h.d, p, piv.data(), &ls[k * TP], &pv[k * DP]);
         } else {
           for (int s = 0; s < h.T; ++s) ls[k * TP + s] = p[s];
           p += h.T;
-          for (int i = 0; i < h.d; ++i) pv[k * DP + i] = (uint8_t)p[i];
+          for (int i = 0; i < h.d; ++i) pv[k * DP + i] = valid ? (uint8_t)p[i] : (uint8_t)i;
         }
       }
       if ((rc = h2d(e, h.Mv, mv)) || (rc = h2d(e, h.Mvv, mvv)) || (rc = h2d(e, h.Ls, ls)) ||
@@ -1485,7 +1506,7 @@ int mmb_grad_evals(mmb_engine* e, int64_t* n) {
 struct mmb_comm {
   std::vector<mmb_engine*> eng;
   std::vector<ncclComm_t> comm;
-  std::vector<double*> buf;  // per local engine: [L stats | 2p range | p shift | p link (int32)]
+  std::vector<double*> buf;  // per local engine: [L stats | 2p range | p shift | p link (int32) | 4 agree]
   int p = 0;
   int64_t L = 0;
 };
@@ -1539,7 +1560,7 @@ int mmb_comm_init(mmb_engine** engines, int nlocal, int nranks, int rank0, const
   c->buf.assign(nlocal, nullptr);
   c->p = e0->pmon;
   c->L = mmb_gr_len(e0);
-  const size_t nbuf = (size_t)c->L + 4 * (size_t)c->p;
+  const size_t nbuf = (size_t)c->L + 4 * (size_t)c->p + 4;
   for (int i = 0; i < nlocal; ++i) {
     if (hipSetDevice(engines[i]->device) != hipSuccess || hipMalloc(&c->buf[i], nbuf * sizeof(double)) != hipSuccess) {
       mmb_comm_destroy(c);
@@ -1579,29 +1600,76 @@ static int comm_sync(mmb_comm* c) {
   return 0;
 }
 
+// One in-place all-reduce of n doubles at offset off of every local engine's buffer, grouped.
+// ncclGroupEnd is called whatever happens inside the group, so a failed call never leaves the
+// thread's RCCL group open for later collectives.
+static ncclResult_t grouped_allreduce(mmb_comm* c, size_t off, size_t n, ncclRedOp_t op) {
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return r;
+  for (size_t i = 0; r == ncclSuccess && i < c->eng.size(); ++i)
+    r = ncclAllReduce(c->buf[i] + off, c->buf[i] + off, n, ncclDouble, op, c->comm[i], c->eng[i]->stream);
+  const ncclResult_t r2 = ncclGroupEnd();
+  return r != ncclSuccess ? r : r2;
+}
+
+// Agreement step before a data collective.  Every local engine contributes (flag, -n_kept,
+// n_kept) to one MAX all-reduce, where flag = 1 if this process cannot take part (too few kept
+// draws on some local engine).  A process whose precondition fails therefore still enters the
+// collective, and every rank sees the same verdict: all fail together (MMB_E_STATE for too few
+// draws, MMB_E_ARG when the ranks kept different numbers of draws, which would otherwise give
+// a silently wrong PSRF) or all proceed with the common n_kept.
+static int comm_agree(mmb_comm* c, int64_t need, int64_t* nkept) {
+  mmb_engine* e0 = c->eng[0];
+  const size_t off = (size_t)c->L + 4 * (size_t)c->p;
+  int64_t lo = INT64_MAX, hi = -1;
+  for (mmb_engine* e : c->eng) { lo = std::min(lo, e->n_kept); hi = std::max(hi, e->n_kept); }
+  const double mine[4] = {lo < need ? 1.0 : 0.0, -(double)lo, (double)hi, 0.0};
+  for (size_t i = 0; i < c->eng.size(); ++i) {
+    HIPCHK(e0, hipSetDevice(c->eng[i]->device));
+    HIPCHK(e0, hipMemcpyAsync(c->buf[i] + off, mine, sizeof(mine), hipMemcpyHostToDevice, c->eng[i]->stream));
+  }
+  const ncclResult_t r = grouped_allreduce(c, off, 4, ncclMax);
+  if (r != ncclSuccess) return fail(e0, MMB_E_COMM, "agreement all-reduce: %s", ncclGetErrorString(r));
+  double all[4];
+  HIPCHK(e0, hipSetDevice(e0->device));
+  HIPCHK(e0, hipMemcpyAsync(all, c->buf[0] + off, sizeof(all), hipMemcpyDeviceToHost, e0->stream));
+  int rc = comm_sync(c);  // also keeps `mine` alive until the H2D copies are done
+  if (rc) return rc;
+  if (all[0] != 0.0)
+    return fail(e0, MMB_E_STATE, "need >= %lld device-kept draws per chain on every rank (this process: %lld)",
+                (long long)need, (long long)lo);
+  if (-all[1] != all[2])
+    return fail(e0, MMB_E_ARG, "ranks kept different numbers of draws (%.0f .. %.0f)", -all[1], all[2]);
+  *nkept = (int64_t)all[2];
+  return 0;
+}
+
 int mmb_range_allreduce(mmb_comm* c, double* minmax) {
   if (!c || !minmax) return fail(nullptr, MMB_E_ARG, "null argument");
   mmb_engine* e0 = c->eng[0];
   const int p = c->p;
+  int64_t nk = 0;
+  int rc = comm_agree(c, 1, &nk);
+  if (rc) return rc;
   for (size_t i = 0; i < c->eng.size(); ++i) {
     mmb_engine* e = c->eng[i];
-    if (e->n_kept < 1) return fail(e0, MMB_E_STATE, "no device-kept draws on engine %zu", i);
     HIPCHK(e0, hipSetDevice(e->device));
     double* mm = c->buf[i] + c->L;
-    hipError_t st = mmb_launch_gr_range(p, e->n_kept, (int)e->K, e->d_draws, mm, e->stream);
-    if (st != hipSuccess) return fail(e0, MMB_E_HIP, "gr_range: %s", hipGetErrorString(st));
-    hipLaunchKernelGGL(mmb_negate_mins, dim3(1), dim3(((p + 63) / 64) * 64), 0, e->stream, mm, p);
-    HIPCHK(e0, hipGetLastError());
+    hipError_t st = mmb_launch_gr_range(p, nk, (int)e->K, e->d_draws, mm, e->stream);
+    if (st == hipSuccess) {
+      hipLaunchKernelGGL(mmb_negate_mins, dim3(1), dim3(((p + 63) / 64) * 64), 0, e->stream, mm, p);
+      st = hipGetLastError();
+    }
+    // a local launch failure after the agreement still joins the all-reduce below (its peers
+    // are already committed to it); the error is reported afterwards
+    if (st != hipSuccess) rc = fail(e0, MMB_E_HIP, "gr_range: %s", hipGetErrorString(st));
   }
-  NCCLCHK(e0, ncclGroupStart());
-  for (size_t i = 0; i < c->eng.size(); ++i) {
-    double* mm = c->buf[i] + c->L;
-    NCCLCHK(e0, ncclAllReduce(mm, mm, 2 * (size_t)p, ncclDouble, ncclMax, c->comm[i], c->eng[i]->stream));
-  }
-  NCCLCHK(e0, ncclGroupEnd());
+  const ncclResult_t r = grouped_allreduce(c, (size_t)c->L, 2 * (size_t)p, ncclMax);
+  if (r != ncclSuccess) return fail(e0, MMB_E_COMM, "range all-reduce: %s", ncclGetErrorString(r));
+  if (rc) return rc;
   HIPCHK(e0, hipSetDevice(e0->device));
   HIPCHK(e0, hipMemcpyAsync(minmax, c->buf[0] + c->L, 2 * p * sizeof(double), hipMemcpyDeviceToHost, e0->stream));
-  int rc = comm_sync(c);
+  rc = comm_sync(c);
   if (rc) return rc;
   for (int j = 0; j < p; ++j) minmax[2 * j] = -minmax[2 * j];
   return 0;
@@ -1611,21 +1679,22 @@ int mmb_gr_allreduce(mmb_comm* c, const int32_t* link, const double* shift, doub
   if (!c || !link || !shift || !out) return fail(nullptr, MMB_E_ARG, "null argument");
   mmb_engine* e0 = c->eng[0];
   const int p = c->p;
+  int64_t nk = 0;
+  int rc = comm_agree(c, 2, &nk);
+  if (rc) return rc;
   for (size_t i = 0; i < c->eng.size(); ++i) {
     mmb_engine* e = c->eng[i];
-    if (e->n_kept < 2) return fail(e0, MMB_E_STATE, "need >= 2 device-kept draws per chain (engine %zu)", i);
     HIPCHK(e0, hipSetDevice(e->device));
     double* ds = c->buf[i] + c->L + 2 * p;
     int32_t* dl = (int32_t*)(ds + p);
-    HIPCHK(e0, hipMemcpyAsync(ds, shift, p * sizeof(double), hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e0, hipMemcpyAsync(dl, link, p * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
-    hipError_t st = mmb_launch_gr_stats(p, e->n_kept, (int)e->K, e->d_draws, dl, ds, c->buf[i], e->stream);
-    if (st != hipSuccess) return fail(e0, MMB_E_HIP, "gr_stats: %s", hipGetErrorString(st));
+    hipError_t st = hipMemcpyAsync(ds, shift, p * sizeof(double), hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(dl, link, p * sizeof(int32_t), hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess) st = mmb_launch_gr_stats(p, nk, (int)e->K, e->d_draws, dl, ds, c->buf[i], e->stream);
+    if (st != hipSuccess) rc = fail(e0, MMB_E_HIP, "gr_stats: %s", hipGetErrorString(st));
   }
-  NCCLCHK(e0, ncclGroupStart());
-  for (size_t i = 0; i < c->eng.size(); ++i)
-    NCCLCHK(e0, ncclAllReduce(c->buf[i], c->buf[i], (size_t)c->L, ncclDouble, ncclSum, c->comm[i], c->eng[i]->stream));
-  NCCLCHK(e0, ncclGroupEnd());
+  const ncclResult_t r = grouped_allreduce(c, 0, (size_t)c->L, ncclSum);
+  if (r != ncclSuccess) return fail(e0, MMB_E_COMM, "Gelman-Rubin all-reduce: %s", ncclGetErrorString(r));
+  if (rc) { (void)comm_sync(c); return rc; }
   HIPCHK(e0, hipSetDevice(e0->device));
   HIPCHK(e0, hipMemcpyAsync(out, c->buf[0], c->L * sizeof(double), hipMemcpyDeviceToHost, e0->stream));
   // the host copies of link/shift must outlive the async H2D copies: wait before returning

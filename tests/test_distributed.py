@@ -5,8 +5,11 @@ rank reduces its chains' kept draws to the L-vector of sufficient statistics, th
 ranks all-reduce it (SUM) plus the link-function range (MAX), and the PSRF comes out
 of the global sums.  Here each rank holds a host shard with the engine's GR interface
 (the device kernel gr_stats_kernel computes the same per-chain quantities; its parity
-with this host form is tests/test_gpu_parity.py::test_gr_device_vs_host).  The
-collectives are the ones bench.py issues over RCCL, run over gloo on CPU.
+with this host form is tests/test_gpu_parity.py::test_device_gelman_rubin_matches_host).
+The collectives are the ones bench.py issues over RCCL, run over gloo on CPU.
+test_library_partials_two_processes (-m gpu) runs the same exchange over the library's own
+device partials: two processes, each an engine over its shard of global chains on the one
+GPU of the box (RCCL refuses two ranks on one device, so the exchange is gloo there).
 """
 import os
 import socket
@@ -126,3 +129,63 @@ def test_sharded_equals_single_process():
         psrf, _ = mb.gelmandiag_sharded(HostShard(d), transform=tr)
         ref, _ = mb.gelmandiag(d, transform=tr)
         np.testing.assert_allclose(psrf, ref, rtol=1e-10)
+
+
+def _gpu_worker(rank, world, port, q, K):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import _mamba_path
+        mb = _mamba_path.load()
+        m = mb.rats()
+        m.setinputs(mb.model.RATS_DATA)
+        m.setsamplers(mb.model.rats_scheme_gibbs_amm())
+        init = mb.model.rats_init_ls(world * K, seed=7)[rank * K:(rank + 1) * K]
+        eng = mb.Engine(m, device=0)
+        eng.init_chains(init, seed=11, chain_offset=rank * K)
+        d = eng.run(120, burnin=40, thin=2, keep_device=True)
+
+        def ar_sum(x):
+            t = torch.tensor(x, dtype=torch.float64)
+            dist.all_reduce(t)
+            return t.numpy()
+
+        def ar_minmax(a, b):
+            t = torch.tensor(np.concatenate([-a, b]), dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t = t.numpy()
+            return -t[:len(a)], t[len(a):]
+
+        out = {tr: mb.gelmandiag_sharded(eng, allreduce_sum=ar_sum, allreduce_minmax=ar_minmax,
+                                         transform=tr, mpsrf=True) for tr in (False, True)}
+        q.put((rank, d, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_library_partials_two_processes():
+    """Two processes x one engine each (global chains [r K, (r+1) K), chain_offset = r K):
+    mmb_gr_range / mmb_gr_partials of each shard, exchanged by all-reduce, give the PSRF of
+    the host gelmandiag over all 2K chains' draws (gelmandiag.jl:11-25)."""
+    import _mamba_path
+    mb = _mamba_path.load()
+    world, K = 2, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, K)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (d, o)) for r, d, o in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    d = np.concatenate([res[r][0] for r in range(world)], axis=2)
+    assert d.shape == (40, 3, world * K)
+    for tr in (False, True):
+        ref, ref_mp = mb.gelmandiag(d, transform=tr, mpsrf=True)
+        for r in range(world):
+            psrf, mp_ = res[r][1][tr]
+            np.testing.assert_allclose(psrf, ref, rtol=1e-8)
+            np.testing.assert_allclose(mp_, ref_mp, rtol=1e-8)

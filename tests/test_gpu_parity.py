@@ -99,15 +99,84 @@ def test_restart_and_sharding(mamba, oracle):
     init = mamba.model.rats_init_ls(128, seed=3)
     e1 = mamba.Engine(m)
     e1.init_chains(init, seed=5)
-    full = e1.run(90, burnin=30, thin=3)
+    full = e1.run(150, burnin=30, thin=3)
     e2 = mamba.Engine(m)
     e2.init_chains(init, seed=5)
-    a = e2.run(40, burnin=30, thin=3)
-    b = e2.run(50, burnin=30, thin=3)
+    a = e2.run(70, burnin=30, thin=3)             # split past AMM's switch at m = 2d + 1 = 61
+    b = e2.run(80, burnin=30, thin=3)
     np.testing.assert_array_equal(np.concatenate([a, b]), full)
     e3 = mamba.Engine(m)
     e3.init_chains(init[64:], chain_offset=64, seed=5)
-    np.testing.assert_array_equal(e3.run(90, burnin=30, thin=3), full[:, :, 64:])
+    np.testing.assert_array_equal(e3.run(150, burnin=30, thin=3), full[:, :, 64:])
+
+
+@pytest.mark.parametrize("how", ["window", "host_roundtrip", "file"])
+def test_rats_carried_proposal_resume_after_switch(mamba, oracle, tmp_path, how):
+    """AMM's carried proposal (samplers.h, tag = host epoch << 32 | iteration) after the
+    adaptive switch (m > 2d = 60, amm.jl:72-76): 256 chains x 200 iterations split at 100
+    (i) into two mmb_run windows with no host write (the carried proposal is reused),
+    (ii) with a values + tune + iter round trip through the host in between (the epoch
+    changes: the first resumed update recomputes SigmaLm z2 by the direct matvec from the
+    factor restored by mmb_set_tune's slot -> position conversion), (iii) through a file
+    checkpoint into a fresh engine (mcmc.jl:3-16).  Each equals the uninterrupted run bit for
+    bit and the oracle within rtol 1e-9."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_ls(256, seed=12)
+    eng, full, st, do = both(mamba, oracle, m, init, 200, 100, 2, seed=21)
+    np.testing.assert_allclose(full, do, rtol=1e-9, atol=1e-9)
+    m1 = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    e1 = mamba.Engine(m1)
+    e1.init_chains(init, seed=21)
+    a = e1.run(100, burnin=100, thin=2)
+    assert a is None
+    tune_mid = e1.tune()
+    amm = [o for o, s in zip(np.cumsum([0] + [len_ for len_ in mamba_tune_lens(mamba, m1)]), m1.samplers)
+           if s.kind == mamba.abi.MMB_SAMPLER_AMM]
+    # m = 100 > 2d: past the switch; most chains hold a valid (full-rank) factor whose carried
+    # proposal the next window uses (the others are rank deficient: SigmaLm is kept, amm.jl:88-90)
+    assert all((tune_mid[:, o + 1] == 100).all() and (tune_mid[:, o + 2] == 1).sum() >= 96 for o in amm)
+    if how == "host_roundtrip":
+        v, t, it = e1.values(), e1.tune(), e1.iter
+        o, d = amm[0], 30
+        bad = t.copy()
+        bad[5, o + 4 + 2 * d + d * (d + 1) - 1] = bad[5, o + 4 + 2 * d + d * (d + 1) - 2]  # repeated pivot
+        with pytest.raises(RuntimeError, match="not a permutation"):
+            e1.set_tune(bad)                                # rejected before any state changes
+        bad = t.copy()
+        bad[7, o + 4 + 2 * d + d * (d + 1) - d] = 30.0      # pivot index out of range
+        with pytest.raises(RuntimeError, match="not a permutation"):
+            e1.set_tune(bad)
+        e1.set_values(v)
+        e1.set_tune(t)
+        e1.set_iter(it)
+        np.testing.assert_array_equal(e1.tune(), t)
+        b = e1.run(100, burnin=100, thin=2)
+    elif how == "file":
+        m1.iter, m1.burnin = e1.iter, 0
+        mc = mamba.Chains(np.empty((0, e1.pmon, 256)), m1.monitor_names, 102, 2, np.arange(1, 257), m1, e1)
+        p = str(tmp_path / "rats_switch.chains")
+        mamba.write(p, mc)
+        e1.close()
+        mc2 = mamba.read(p, model=rats(mamba, mamba.model.rats_scheme_gibbs_amm()))
+        assert mc2.engine.iter == 100
+        b = mc2.engine.run(100, burnin=100, thin=2)
+    else:
+        b = e1.run(100, burnin=100, thin=2)
+    np.testing.assert_array_equal(b, full)
+
+
+def mamba_tune_lens(mamba, m):
+    """Canonical tune-row length of each block (engine.cpp mmb_get_tune layout)."""
+    out = []
+    for s in m.samplers:
+        d = m.block_dim(s)
+        if s.kind == mamba.abi.MMB_SAMPLER_AMWG:
+            out.append(2 + 2 * d)
+        elif s.kind == mamba.abi.MMB_SAMPLER_AMM:
+            out.append(4 + 2 * d + d * (d + 1))
+        else:
+            out.append(0)
+    return out
 
 
 def test_device_gelman_rubin_matches_host(mamba):
@@ -252,11 +321,11 @@ def test_checkpoint_file_resume(mamba, tmp_path, scheme):
     m = rats(mamba, sch())
     e = mamba.Engine(m)
     e.init_chains(init, chain_offset=32, seed=11)
-    full = e.run(70, burnin=20, thin=2)
+    full = e.run(110, burnin=20, thin=2)
     m1 = rats(mamba, sch())
     e1 = mamba.Engine(m1)
     e1.init_chains(init, chain_offset=32, seed=11)
-    a = e1.run(30, burnin=20, thin=2)
+    a = e1.run(70, burnin=20, thin=2)             # past AMM's adaptive switch (m > 2d = 60)
     m1.iter, m1.burnin = e1.iter, 20
     mc = mamba.Chains(a, m1.monitor_names, 22, 2, np.arange(33, 129), m1, e1)
     p = str(tmp_path / "rats.chains")
@@ -264,10 +333,10 @@ def test_checkpoint_file_resume(mamba, tmp_path, scheme):
     e1.close()
     m2 = rats(mamba, sch())
     mc2 = mamba.read(p, model=m2)
-    assert mc2.engine.iter == 30
+    assert mc2.engine.iter == 70
     mc3 = mamba.mcmc_restart(mc2, 40)
     np.testing.assert_array_equal(mc3.value, full)
-    assert list(mc3.range) == list(range(22, 71, 2))
+    assert list(mc3.range) == list(range(22, 111, 2))
 
 
 @pytest.mark.parametrize("name", ["nuts_slice", "amwg", "hmc", "mala_sigma_gibbs"])
@@ -472,6 +541,29 @@ def test_gr_allreduce_rccl_one_gpu(mamba, how):
     shift = np.array([3.6, 6.0, 100.0])
     np.testing.assert_array_equal(comm.gr_allreduce(kinds, shift), eng.gr_partials(kinds, shift))
     comm.close()
+
+
+def test_gr_allreduce_agreement_fails_together(mamba):
+    """The collective's agreement step (engine.cpp comm_agree): a process whose engines hold
+    too few kept draws fails with MMB_E_STATE *after* joining one MAX all-reduce (its peers
+    do not block), and the RCCL group is closed afterwards: the next collectives on the
+    same communicator still work."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(128, seed=3), seed=4)
+    eng.run(12, burnin=10, thin=2, keep_device=True)        # one kept draw per chain
+    assert eng.num_kept() == 1
+    comm = mamba.Comm([eng], nranks=1, rank0=0, uid=mamba.Comm.unique_id())
+    mm = comm.range_allreduce()                               # needs >= 1: fine
+    np.testing.assert_array_equal(mm, eng.gr_range())
+    with pytest.raises(RuntimeError, match=r"error -4 .*need >= 2 device-kept draws"):
+        comm.gr_allreduce(np.zeros(3, np.int32), np.zeros(3))
+    d = eng.run(40, burnin=0, thin=2, keep_device=True)
+    np.testing.assert_array_equal(comm.range_allreduce(), eng.gr_range())
+    kinds, shift = np.array([1, 0, 0], np.int32), np.array([3.6, 6.0, 100.0])
+    np.testing.assert_array_equal(comm.gr_allreduce(kinds, shift), eng.gr_partials(kinds, shift))
+    comm.close()
+    assert d.shape[0] == 20
 
 
 def test_rats_scale_total_on_one_gpu(mamba, oracle):
