@@ -231,9 +231,11 @@ def test_rats_gibbs_amm_statistical(mamba, oracle, adapt):
     three monitored values match rats.rst:43-52.  With adapt=:all (the headline workload)
     mu_beta and alpha0 match, while s2_c sits low: the always-adapting proposal of
     amm.jl:73-91 starts from a covariance estimated on 2n+1 autocorrelated draws and stays
-    too small for thousands of iterations; tools/amm_numpy_check.py (an independent numpy
-    restatement) reproduces the drop, and tests/test_gpu_rats_long.py pins it at the rats.rst
-    run length.  Here s2_c must lie in the window that run shows."""
+    too small for thousands of iterations; tests/golden/make_rats_amm_restatement.py (an
+    independent numpy restatement) reproduces the drop (tests/golden/rats_amm_restatement.json:
+    34.53 at the rats.rst run length), and tests/test_gpu_rats_long.py holds the GPU to it.
+    Here, 16 oracle chains x 2500 iterations, s2_c must lie in the wide window of that
+    shorter run."""
     pub = load("rats_published.json")
     G = mamba.Gibbs
     sch = (mamba.model.rats_scheme_gibbs_amm() if adapt == "all" else
