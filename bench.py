@@ -41,6 +41,10 @@ CHAINS_PER_GPU = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (spec, dense)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_rats_gibbs_amm_hbm_traffic.json")
+F64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (spec)
+# FP64 VALU lane-flops per chain-update of the reference Slice+AMWG scheme (its binding roofline,
+# SURVEY §8(d) row 3'), from the committed rocprofv3 SQ_INSTS_VALU_*_F64 pass
+VALU_FILE = os.path.join(ROOT, "profiles", "r3_rats_reference_valu_flops.json")
 
 
 def parse():
@@ -367,6 +371,16 @@ def main():
                 "avg_launch_ms": avg_ms, "launches": launches, "chain_updates_per_launch": units / launches}
         if tsrc:
             roof["traffic_source"] = tsrc
+        if args.workload == "rats" and args.scheme == "reference" and os.path.exists(VALU_FILE):
+            # f1 row: bound by FP64 vector issue, not HBM (SURVEY §8(d) row 3'); HBM kept alongside
+            v = json.load(open(VALU_FILE))
+            flops = v["f64_lane_flops_per_chain_update"] * units / launches
+            tfs = flops / (avg_ms * 1e-3) / 1e12
+            hbm = {k: roof[k] for k in ("achieved", "peak", "unit", "frac")}
+            roof.update({"bound": "valu", "achieved": tfs, "peak": F64_VALU_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": tfs / F64_VALU_PEAK_TFS, "hbm": hbm,
+                         "f64_lane_flops_per_chain_update": v["f64_lane_flops_per_chain_update"],
+                         "flops_source": os.path.relpath(VALU_FILE, ROOT)})
     roof["timed_window_kernel_ms_per_step"] = kernel_ms_per_step
     roof["timed_window_launches"] = t_launches
 
@@ -397,7 +411,9 @@ def main():
         out["metric"] = f"chain-updates/sec on {args.workload} (not the headline metric)"
     if args.workload == "rats":
         out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8")),
-                              "amm_adapt": "all"})
+                              "scheme": args.scheme})
+        if args.scheme == "gibbs_amm":
+            out["config"]["amm_adapt"] = "all"
     if nuts_timed is not None:
         out["nuts"] = nuts_timed
     if psrf is not None:

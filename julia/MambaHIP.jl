@@ -13,6 +13,7 @@
 module MambaHIP
 
 using Mamba
+import Distributions
 import Distributions: Univariate, Multivariate
 import Mamba: Model, Sampler, ModelState, ModelChains, Chains, AMWGTune, AMMTune, NUTSTune,
               SliceTune, HMCTune, MALATune, SamplerTune, relist!, unlist, gettune
@@ -175,7 +176,7 @@ function model_kind(m::Model)
   ks == Set([:y, :alpha, :alpha0, :mu_alpha, :s2_alpha, :beta, :mu_beta, :s2_beta, :s2_c]) &&
     return MMB_MODEL_RATS
   ks == Set([:y, :p, :beta]) && return MMB_MODEL_LOGISTIC
-  nothing                                           # any other DAG: lower_ir (below)
+  nothing                                           # any other DAG: lower_ir (node IR, below)
 end
 
 node_id(kind, key::Symbol) = (for (k, id, _) in LAYOUT[kind]; k == key && return id; end; nothing)
@@ -244,6 +245,327 @@ function lower(m::Model)
   ncoef = kind == MMB_MODEL_LOGISTIC ? length(m[:beta].value) : 0
   prior_sd = kind == MMB_MODEL_LOGISTIC ? sqrt(m[:beta].distr.Σ.value) : 0.0
   (ModelSpec(kind, length(m.samplers), tuple(blocks...), nobs, ncoef, prior_sd, ntuple(_ -> Int32(0), 8)), keep)
+end
+
+# ---- node IR lowering (any other Model: MMB_MODEL_IR, mmb_create_ir; INTEGRATION.md §2a) ------
+# Mirror: mamba.jl_amd/ir.py.  Each node's own function (node.eval, src/model/dependent.jl:75-
+# 152, src/utils.jl:3-43) is called once on a tracer Model whose sampled Stochastic nodes are
+# arrays of scalar expression trees (element k of node s = TElem(s, k)), whose inputs and
+# fixed (unsampled) Stochastic nodes are their actual values, and whose Logical nodes hold
+# the trees their own functions return (so Logicals are inlined).  Node functions run
+# unchanged: `alpha[rat] + beta[rat] .* Xm`, `xmat * beta`, `UnivariateDistribution[...
+# for i in 1:N]` comprehensions all evaluate to per-element trees, because TExpr is a Number
+# whose arithmetic records itself.  The per-element trees of a node parameter are then
+# anti-unified into ONE elementwise expression of the IR (element i: CONST, VAL, VALI, VALG
+# gathers, DATA vectors) -- the broadcast form mmb_ir_node expects.  Anything else (a closure
+# that branches on a node value, a distribution outside the IR's families, a partial monitor,
+# a user Gibbs closure) raises inside the trace or the unification and `lower_ir` returns
+# `nothing`: the unchanged Julia path runs.
+const MMB_MODEL_IR = Int32(4)
+const MMB_IR_NORMAL, MMB_IR_ISONORMAL, MMB_IR_INVGAMMA, MMB_IR_GAMMA = Int32(1), Int32(2), Int32(3), Int32(4)
+const MMB_IR_EXPONENTIAL, MMB_IR_UNIFORM, MMB_IR_BETA = Int32(5), Int32(6), Int32(7)
+const MMB_IR_BINOMIAL, MMB_IR_POISSON, MMB_IR_BERNOULLI, MMB_IR_LOGICAL = Int32(8), Int32(9), Int32(10), Int32(11)
+const IR_OP = Dict(:end => 0, :const => 1, :val => 2, :vali => 3, :valg => 4, :data => 5, :datas => 6,
+                   :+ => 16, :- => 17, :* => 18, :/ => 19,
+                   :neg => 32, :exp => 33, :log => 34, :sqrt => 35, :invlogit => 36, :logit => 37, :abs => 38)
+const MMB_IR_MAX_STACK, MMB_IR_MAX_TERMS, MMB_IR_MAX_VALUES = 16, 16, 512
+const IR_SAMPLEABLE = [MMB_IR_NORMAL, MMB_IR_ISONORMAL, MMB_IR_INVGAMMA, MMB_IR_GAMMA, MMB_IR_EXPONENTIAL,
+                       MMB_IR_UNIFORM, MMB_IR_BETA]
+const IR_DISCRETE = [MMB_IR_BINOMIAL, MMB_IR_POISSON, MMB_IR_BERNOULLI]
+
+immutable IrNode                         # mmb_ir_node
+  family::Int32; fixed::Int32; off::Int32; len::Int32
+  expr::NTuple{3,Int32}; cterm::Int32; lo::Float64; hi::Float64
+end
+immutable IrBlock                        # mmb_ir_block
+  nterms::Int32; term::NTuple{16,Int32}; trans::NTuple{16,Int32}
+end
+const NOIRBLOCK = IrBlock(0, ntuple(_ -> Int32(0), 16), ntuple(_ -> Int32(0), 16))
+immutable IrModel                        # mmb_ir_model
+  nvalues::Int32; nnodes::Int32; nodes::Ptr{IrNode}; ncode::Int32; code::Ptr{Int32}
+  nconst::Int32; consts::Ptr{Float64}; npool::Int64; pool::Ptr{Float64}
+  nmon::Int32; mon::Ptr{Int32}; stack::Int32; blocks::NTuple{8,IrBlock}
+end
+
+function create_ir(spec::ModelSpec, ir::IrModel, device::Integer)
+  h = Ref{Ptr{Void}}(C_NULL)
+  rc = ccall((:mmb_create_ir, libmambahip), Cint, (Ref{ModelSpec}, Ref{IrModel}, Cint, Ref{Ptr{Void}}),
+             spec, ir, device, h)
+  rc == MMB_E_UNSUPPORTED && return nothing
+  check(rc, C_NULL); h[]
+end
+
+# -- tracer: scalar expression trees ---------------------------------------------------------
+abstract TExpr <: Number
+immutable TConst <: TExpr; v::Float64; end
+immutable TElem <: TExpr; node::Symbol; k::Int; end       # element k (1-based) of a sampled node
+immutable TBin <: TExpr; op::Symbol; a::TExpr; b::TExpr; end
+immutable TUn <: TExpr; op::Symbol; a::TExpr; end
+
+Base.convert(::Type{TExpr}, x::Real) = TConst(Float64(x))
+Base.convert(::Type{TExpr}, x::TExpr) = x
+Base.promote_rule{S<:TExpr, T<:Real}(::Type{S}, ::Type{T}) = TExpr
+Base.promote_rule{S<:TExpr, T<:TExpr}(::Type{S}, ::Type{T}) = TExpr
+Base.zero{T<:TExpr}(::Type{T}) = TConst(0.0)             # generic matmul / sum start
+Base.zero(::TExpr) = TConst(0.0)
+for op in (:+, :-, :*, :/)
+  @eval Base.$op(a::TExpr, b::TExpr) = TBin($(QuoteNode(op)), a, b)
+end
+Base.:-(a::TExpr) = TUn(:neg, a)
+Base.:+(a::TExpr) = a
+Base.:^(a::TExpr, p::Integer) = p == 2 ? a * a : throw(ArgumentError("node IR: only x^2"))
+for f in (:exp, :log, :sqrt, :abs)
+  @eval Base.$f(a::TExpr) = TUn($(QuoteNode(f)), a)
+end
+Mamba.invlogit(a::TExpr) = TUn(:invlogit, a)              # src/utils.jl:64
+Mamba.logit(a::TExpr) = TUn(:logit, a)                    # src/utils.jl:67
+
+# -- tracer: distributions of traced parameters -----------------------------------------------
+immutable TDist
+  fam::Int32
+  p::Vector{Any}                        # per parameter: a scalar (TExpr or Real) or a vector of them
+end
+typealias TR Union{TExpr, Real}
+import Distributions: Normal, MvNormal, InverseGamma, Gamma, Exponential, Uniform, Beta, Binomial,
+                      Poisson, Bernoulli, ScalMat
+# (Real, Real) arguments keep Distributions' own, more specific methods
+Normal(mu::TR, s::TR) = TDist(MMB_IR_NORMAL, Any[mu, s])
+Normal(mu::TExpr) = TDist(MMB_IR_NORMAL, Any[mu, 1.0])
+InverseGamma(a::TR, b::TR) = TDist(MMB_IR_INVGAMMA, Any[a, b])
+Gamma(a::TR, b::TR) = TDist(MMB_IR_GAMMA, Any[a, b])
+Exponential(b::TExpr) = TDist(MMB_IR_EXPONENTIAL, Any[b])
+Uniform(a::TR, b::TR) = TDist(MMB_IR_UNIFORM, Any[a, b])
+Beta(a::TR, b::TR) = TDist(MMB_IR_BETA, Any[a, b])
+Binomial(n::Real, p::TExpr) = TDist(MMB_IR_BINOMIAL, Any[n, p])
+Poisson(l::TExpr) = TDist(MMB_IR_POISSON, Any[l])
+Bernoulli(p::TExpr) = TDist(MMB_IR_BERNOULLI, Any[p])
+MvNormal{T<:TExpr}(mu::AbstractVector{T}, s::Real) = TDist(MMB_IR_ISONORMAL, Any[mu, s])
+MvNormal(mu::AbstractVector, s::TExpr) = TDist(MMB_IR_ISONORMAL, Any[mu, s])
+MvNormal(k::Integer, s::TExpr) = TDist(MMB_IR_ISONORMAL, Any[0.0, s])
+
+"A distribution object of constant parameters (no tracer reached it) as a TDist."
+function as_tdist(d)
+  isa(d, TDist) && return d
+  params = Distributions.params
+  isa(d, Normal) && return TDist(MMB_IR_NORMAL, Any[params(d)...])
+  isa(d, InverseGamma) && return TDist(MMB_IR_INVGAMMA, Any[params(d)...])
+  isa(d, Gamma) && return TDist(MMB_IR_GAMMA, Any[params(d)...])
+  isa(d, Exponential) && return TDist(MMB_IR_EXPONENTIAL, Any[params(d)...])
+  isa(d, Uniform) && return TDist(MMB_IR_UNIFORM, Any[params(d)...])
+  isa(d, Beta) && return TDist(MMB_IR_BETA, Any[params(d)...])
+  isa(d, Binomial) && return TDist(MMB_IR_BINOMIAL, Any[params(d)...])
+  isa(d, Poisson) && return TDist(MMB_IR_POISSON, Any[params(d)...])
+  isa(d, Bernoulli) && return TDist(MMB_IR_BERNOULLI, Any[params(d)...])
+  if isa(d, MvNormal) && isa(d.Σ, ScalMat)                 # IsoNormal (PDMats ScalMat)
+    return TDist(MMB_IR_ISONORMAL, Any[Float64[mean(d)...], sqrt(d.Σ.value)])
+  end
+  throw(ArgumentError("node IR: distribution $(typeof(d)) is not lowered"))
+end
+
+# -- anti-unification of per-element trees into one elementwise IR expression ------------------
+# IR expression: (:const, v) | (:val, slot) | (:vali, off) | (:valg, off, idx0) | (:data, vec) |
+#                (op, a, b) | (op, a)
+function vectorize(ts::Vector, L)                # L: the IR lowering state
+  n = length(ts)
+  t = map(x -> isa(x, Real) ? TConst(Float64(x)) : x, ts)
+  isa(t[1], TExpr) || throw(ArgumentError("node IR: a parameter is not arithmetic"))
+  if all(x -> isa(x, TConst), t)
+    v = Float64[x.v for x in t]
+    return all(x -> x == v[1], v) ? (:const, v[1]) : (:data, v)
+  elseif all(x -> isa(x, TElem), t)
+    s = t[1].node
+    all(x -> x.node == s, t) || throw(ArgumentError("node IR: elements of different nodes in one position"))
+    ks = Int[x.k for x in t]
+    off = L.slot[s]
+    all(k -> k == ks[1], ks) && return (:val, off + ks[1] - 1)
+    ks == collect(1:n) && L.len[s] == n && return (:vali, off)
+    return (:valg, off, Float64[k - 1 for k in ks])
+  elseif all(x -> isa(x, TBin), t)
+    op = t[1].op
+    all(x -> x.op == op, t) || throw(ArgumentError("node IR: elements differ in an operation"))
+    return (op, vectorize(Any[x.a for x in t], L), vectorize(Any[x.b for x in t], L))
+  elseif all(x -> isa(x, TUn), t)
+    op = t[1].op
+    all(x -> x.op == op, t) || throw(ArgumentError("node IR: elements differ in an operation"))
+    return (op, vectorize(Any[x.a for x in t], L))
+  end
+  throw(ArgumentError("node IR: elements of a parameter do not share one expression"))
+end
+
+"Elementwise trees of parameter `p` for an n-element node: a scalar is shared by every element."
+per_element(p, n) = isa(p, AbstractArray) ? (length(p) == n ? Any[p...] :
+                      throw(ArgumentError("node IR: parameter length $(length(p)) for $n elements"))) : Any[p]
+
+type IrLowering
+  slot::Dict{Symbol,Int}; len::Dict{Symbol,Int}
+  code::Vector{Int32}; consts::Vector{Float64}; pool::Vector{Float64}; depth::Int
+end
+
+word(op::Symbol, arg::Integer) = (0 <= arg < 1 << 24 ||
+  throw(ArgumentError("node IR operand $arg does not fit in 24 bits")); Int32(IR_OP[op] << 24 | arg))
+function pool!(L::IrLowering, v::Vector{Float64})
+  off = length(L.pool); append!(L.pool, v); off
+end
+function emit!(L::IrLowering, e, sp::Int)
+  push(w) = (push!(L.code, w); L.depth = max(L.depth, sp + 1); sp + 1)
+  k = e[1]
+  if k == :const
+    push!(L.consts, e[2]); return push(word(:const, length(L.consts) - 1))
+  elseif k == :val
+    return push(word(:val, e[2]))
+  elseif k == :vali
+    return push(word(:vali, e[2]))
+  elseif k == :valg
+    sp2 = push(word(:valg, e[2])); push!(L.code, Int32(pool!(L, e[3]))); return sp2
+  elseif k == :data
+    return push(word(:data, pool!(L, e[2])))
+  elseif length(e) == 3
+    sp = emit!(L, e[2], sp); sp = emit!(L, e[3], sp); push!(L.code, word(k, 0)); return sp - 1
+  end
+  sp = emit!(L, e[2], sp); push!(L.code, word(k, 0)); sp
+end
+function expr!(L::IrLowering, e)
+  start = length(L.code)
+  emit!(L, e, 0)
+  push!(L.code, Int32(0))                 # END
+  Int32(start)
+end
+host_const(e) = e[1] == :const ? e[2] : throw(ArgumentError("node IR: a bound must be a constant"))
+host_data(e, n) = e[1] == :const ? fill(e[2], n) : e[1] == :data ? e[2] :
+                  throw(ArgumentError("node IR: Binomial n must be data"))
+
+"""
+    lower_ir(m) -> (ModelSpec, IrModel, layout, keep) or nothing
+
+Walks m.nodes (src/model/dependent.jl:75-152, model.jl:5-27) into an mmb_ir_model.  `layout`
+lists (node, length) of the sampled nodes in the order of their state slots: the engine value
+row of a chain.  Term lists per block are the reference's own: `keys(m, :block, b)` minus the
+targets, then the Stochastic nodes of `keys(m, :target, b)` (simulation.jl:79-88).
+"""
+function lower_ir(m::Model)
+  try
+    return lower_ir_(m)
+  catch err
+    isa(err, ArgumentError) || isa(err, MethodError) || isa(err, BoundsError) || rethrow(err)
+    return nothing                       # not lowerable: the Julia path
+  end
+end
+
+function lower_ir_(m::Model)
+  length(m.samplers) > 8 && return nothing
+  deps = keys(m, :dependent)            # tsorted Logical + Stochastic keys
+  inblock = Set(vcat([s.params for s in m.samplers]...))
+  stoch = filter(k -> isa(m[k], Mamba.AbstractStochastic), deps)
+  sampled = filter(k -> k in inblock, stoch)
+  L = IrLowering(Dict{Symbol,Int}(), Dict{Symbol,Int}(), Int32[], Float64[], Float64[], 1)
+  off = 0
+  for k in sampled                       # state slots: sampled nodes in dependent order
+    L.slot[k], L.len[k] = off, length(m[k].value); off += L.len[k]
+  end
+  1 <= off <= MMB_IR_MAX_VALUES || throw(ArgumentError("node IR: 1..$MMB_IR_MAX_VALUES sampled values"))
+  # tracer model: sampled nodes -> element trees, inputs / fixed nodes -> their values
+  tm = Model(Dict{Symbol,Any}(), Sampler[], ModelState[], 0, 0, false, false)
+  for (k, v) in m.nodes
+    if k in inblock
+      tm.nodes[k] = isa(v.value, AbstractArray) ?
+        reshape(TExpr[TElem(k, i) for i in 1:length(v.value)], size(v.value)) : TElem(k, 1)
+    else
+      tm.nodes[k] = isa(v, Mamba.AbstractDependent) ? v.value : v
+    end
+  end
+  for k in deps                          # Logicals inlined, in topological order
+    isa(m[k], Mamba.AbstractLogical) && (tm.nodes[k] = m[k].eval(tm))
+  end
+  ids = Dict(k => Int32(i - 1) for (i, k) in enumerate(deps))
+  nodes = IrNode[]
+  for k in deps
+    node = m[k]
+    n = length(node.value)
+    ex = Int32[-1, -1, -1]
+    if isa(node, Mamba.AbstractLogical)
+      val = tm.nodes[k]
+      ex[1] = expr!(L, vectorize(per_element(isa(val, AbstractArray) ? vec(val) : val, n), L))
+      push!(nodes, IrNode(MMB_IR_LOGICAL, 0, 0, n, (ex...), -1, 0.0, 0.0)); continue
+    end
+    d = node.eval(tm)                    # TDist, a Distribution, or an array of them (per element)
+    if isa(d, AbstractArray)
+      ds = map(as_tdist, vec(d))
+      length(ds) == n || throw(ArgumentError("node IR: $k has $(length(ds)) distributions for $n elements"))
+      fam = ds[1].fam
+      all(x -> x.fam == fam, ds) || throw(ArgumentError("node IR: $k mixes distribution families"))
+      np = length(ds[1].p)
+      par = [Any[x.p[j] for x in ds] for j in 1:np]          # parameter j, element i
+    else
+      dd = as_tdist(d)
+      fam = dd.fam
+      par = fam == MMB_IR_ISONORMAL ?
+        Any[per_element(dd.p[1] == 0.0 ? 0.0 : dd.p[1], isa(dd.p[1], AbstractArray) ? n : 1), Any[dd.p[2]]] :
+        [per_element(p, isa(p, AbstractArray) ? n : 1) for p in dd.p]
+    end
+    fixed = !(k in inblock)
+    fixed || fam in IR_SAMPLEABLE || throw(ArgumentError("node IR: $k cannot be sampled by these samplers"))
+    vecs = Any[vectorize(p, L) for p in par]
+    for (j, e) in enumerate(vecs); ex[j] = expr!(L, e); end
+    x = Float64[node.value...]
+    lo = hi = 0.0
+    cterm = Int32(-1)
+    if fam == MMB_IR_UNIFORM
+      lo, hi = host_const(vecs[1]), host_const(vecs[2])
+    elseif fam in IR_DISCRETE
+      fixed || throw(ArgumentError("node IR: discrete node $k cannot be sampled"))
+      all(v -> v == round(v) && v >= 0, x) || throw(ArgumentError("node IR: $k: counts must be integers >= 0"))
+      if fam == MMB_IR_BINOMIAL
+        nn = host_data(vecs[1], n)
+        cterm = Int32(pool!(L, Float64[lgamma(a + 1) - lgamma(b + 1) - lgamma(a - b + 1) for (a, b) in zip(nn, x)]))
+      elseif fam == MMB_IR_POISSON
+        cterm = Int32(pool!(L, Float64[-lgamma(b + 1) for b in x]))
+      end
+    end
+    o = fixed ? pool!(L, x) : L.slot[k]
+    push!(nodes, IrNode(fam, fixed ? 1 : 0, o, n, (ex...), cterm, lo, hi))
+  end
+  L.depth <= MMB_IR_MAX_STACK || throw(ArgumentError("node IR: expression too deep"))
+  # blocks: BlockSpec from the sampler registry, term list of logpdf! (simulation.jl:79-88)
+  blocks, irb, keep = fill(NOBLOCK, 8), fill(NOIRBLOCK, 8), Any[nodes, L]
+  for (b, s) in enumerate(m.samplers)
+    length(s.params) > 4 && return nothing
+    pids = Int32[ids[p] for p in s.params]
+    dim = sum(p -> L.len[p], s.params)
+    dim <= 32 || throw(ArgumentError("node IR: blocks of at most 32 elements"))
+    sp = block_spec(s, ntuple(i -> i <= length(pids) ? pids[i] : Int32(0), 4), length(pids), dim, keep)
+    sp === nothing && return nothing
+    blocks[b] = sp
+    targets = filter(k -> isa(m[k], Mamba.AbstractStochastic), keys(m, :target, b))
+    terms = vcat(setdiff(s.params, targets), targets)
+    length(terms) <= MMB_IR_MAX_TERMS || throw(ArgumentError("node IR: too many nodes in one logpdf!"))
+    irb[b] = IrBlock(length(terms), ntuple(i -> i <= length(terms) ? ids[terms[i]] : Int32(0), 16),
+                     ntuple(i -> i <= length(terms) ? Int32(terms[i] in s.params) : Int32(0), 16))
+  end
+  # monitored nodes in names(m, true) order (model.jl:231-239): whole nodes only
+  mon = Int32[]
+  for k in deps
+    mk = m[k].monitor
+    isempty(mk) && continue
+    mk == collect(1:length(m[k].value)) || throw(ArgumentError("node IR: partial monitor of $k"))
+    push!(mon, ids[k])
+  end
+  code, consts, pool = L.code, vcat(L.consts, 0.0), vcat(L.pool, 0.0)
+  append!(keep, Any[code, consts, pool, mon])
+  ir = IrModel(off, length(nodes), pointer(nodes), length(code), pointer(code), length(L.consts),
+               pointer(consts), length(L.pool), pointer(pool), length(mon), pointer(mon), L.depth, (irb...))
+  spec = ModelSpec(MMB_MODEL_IR, length(m.samplers), (blocks...), 0, 0, 0.0, ntuple(_ -> Int32(0), 8))
+  layout = [(k, L.len[k]) for k in sampled]
+  (spec, ir, layout, keep)
+end
+
+"One chain's engine value row of a node-IR model (layout from lower_ir)."
+ir_values(m::Model, layout) = vcat([Float64[m[k].value...] for (k, _) in layout]...)
+function set_ir_values!(m::Model, layout, v::AbstractVector{Float64})
+  o = 0
+  for (k, n) in layout
+    m[k].value = isa(m[k].value, AbstractArray) ? reshape(v[o + (1:n)], size(m[k].value)) : v[o + 1]
+    o += n
+  end
 end
 
 "setinputs! data the kernels read (names of include/mamba_hip.h mmb_set_data)."
@@ -351,14 +673,14 @@ function pack_tunes(m::Model, states::Vector{ModelState}, iter::Integer)
 end
 
 "m.states[k] = ModelState(values, tune) from the engine after a window (mcmc.jl:54-56, 82)."
-function store_states!(m::Model, e, kind, states::Vector{ModelState})
+function store_states!(m::Model, e, setvals!::Function, states::Vector{ModelState})
   K = length(states)
   vals = Array{Float64}(num_values(e), K); get_values!(e, vals)
   TL = tune_len(e)
   tunes = Array{Float64}(TL, K)
   TL > 0 && get_tune!(e, tunes)
   for k in 1:K
-    set_engine_values!(m, kind, vals[:, k])
+    setvals!(vals[:, k])
     tune = deepcopy(states[k].tune)
     o = 0
     for (b, s) in enumerate(m.samplers)
@@ -376,24 +698,38 @@ end
 """
     run_chains!(m, window, burnin, thin, chains; device=0, seed=...) -> ModelChains or nothing
 
-The GPU path of `mcmc_master!`: `nothing` when `lower(m)` does not recognise the model or a
-block (the caller then runs `pmap2(mcmc_worker!, lsts)` unchanged).  Global chain id of
+The GPU path of `mcmc_master!`: `nothing` when neither `lower(m)` (the hand-lowered line /
+rats / logistic kinds) nor `lower_ir(m)` (any other DAG, the node IR) takes the model and its
+blocks (the caller then runs `pmap2(mcmc_worker!, lsts)` unchanged).  Global chain id of
 chains[k] is chains[k] - 1, so a chain's Philox streams (and its draws) do not depend on
 how chains are split over calls or GPUs.
 """
 function run_chains!(m::Model, window::UnitRange{Int}, burnin::Integer, thin::Integer,
                      chains::AbstractArray{Int}; device::Integer=0, seed::UInt64=UInt64(20261015))
   low = lower(m)
-  low === nothing && return nothing
-  spec, keep = low
-  kind = spec.model
-  e = create(spec, device)
+  if low !== nothing
+    spec, keep = low
+    kind = spec.model
+    getvals = () -> engine_values(m, kind)
+    setvals! = v -> set_engine_values!(m, kind, v)
+    e = create(spec, device)
+  else
+    irl = lower_ir(m)                                  # the node IR (mmb_create_ir)
+    irl === nothing && return nothing
+    spec, ir, layout, keep = irl
+    kind = MMB_MODEL_IR
+    getvals = () -> ir_values(m, layout)
+    setvals! = v -> set_ir_values!(m, layout, v)
+    e = create_ir(spec, ir, device)
+  end
   e === nothing && return nothing
   try
-    for (name, x) in inputs(m, kind); set_data!(e, name, x); end
+    if kind != MMB_MODEL_IR                            # (the node IR carries its data in the pool)
+      for (name, x) in inputs(m, kind); set_data!(e, name, x); end
+    end
     states = m.states
     length(states) == length(chains) || throw(ArgumentError("one ModelState per chain expected"))
-    init = hcat([(relist!(m, st.value); engine_values(m, kind)) for st in states]...)   # P x K
+    init = hcat([(relist!(m, st.value); getvals()) for st in states]...)   # P x K
     offset = first(chains) - 1
     chains == offset + (1:length(chains)) || throw(ArgumentError("chains must be a contiguous range"))
     init_chains!(e, init, offset, seed)
@@ -413,7 +749,7 @@ function run_chains!(m::Model, window::UnitRange{Int}, burnin::Integer, thin::In
     size(sim.value, 2) == num_monitored(e) || return nothing   # monitor flags the engine does not lower
     a = RunArgs(length(window), burnin, thin, m.burnin, nkept == 0 ? Ptr{Float64}(C_NULL) : pointer(sim.value), 0, 0)
     run!(e, a)                                         # writes n x p x K in Chains order
-    store_states!(m, e, kind, states)
+    store_states!(m, e, setvals!, states)
     m.iter = last(window)
     return ModelChains(sim, m)
   finally

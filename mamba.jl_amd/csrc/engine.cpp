@@ -577,6 +577,13 @@ void mmb_destroy(mmb_engine* e) {
 #ifdef MMB_PHASE_PROF
   mmb_prof_dump();
 #endif
+#ifdef MMB_PCHOL_COUNT
+  if (e->d_nstat) {
+    unsigned long long v[8];
+    if (hipMemcpy(v, e->d_nstat, sizeof v, hipMemcpyDeviceToHost) == hipSuccess)
+      fprintf(stderr, "MMB_PCHOL exact-path steps %llu\n", v[4]);
+  }
+#endif
   free_dev(e);
   if (e->d_data) (void)hipFree(e->d_data);
   {
@@ -782,8 +789,8 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
   e->n_kept = 0;
   HIPCHK(e, dalloc(&e->d_vals, (size_t)K * e->VS));
   e->slice_overflows = 0;
-  HIPCHK(e, dalloc(&e->d_nstat, 4));
-  HIPCHK(e, hipMemset(e->d_nstat, 0, 4 * sizeof(unsigned long long)));
+  HIPCHK(e, dalloc(&e->d_nstat, 8));  // [4]: pchol32 exact-path steps (-DMMB_PCHOL_COUNT builds)
+  HIPCHK(e, hipMemset(e->d_nstat, 0, 8 * sizeof(unsigned long long)));
   const size_t DP = e->DP, TP = e->TP;
   for (auto& h : e->blocks) {
     HIPCHK(e, dalloc(&h.m, K));

@@ -382,6 +382,21 @@ struct Smp {
                                                 int* pos_out, const DBlock* NB = nullptr,
                                                 const SweepArgs& A = SweepArgs{}, int c = 0, uint32_t chain = 0,
                                                 int64_t it = 0, int b = 0, int m = 0) {
+    return pchol32_impl<true>(d, mat, prow, pks, pos_out, NB, A.seed, A.xepoch, c, chain, it, b, m);
+  }
+#if !defined(MMB_PCHOL_V1) && defined(MMB_PCHOL_EXACT_NOINLINE)
+  // timing experiment: the checked pass (rare) out of line (measured 13 % slower: call ABI)
+  __device__ __noinline__ static int pchol32_exact(int d, double* mat, double* prow, int* pks, int* pos_out,
+                                                   const DBlock* NB, uint64_t seed, int64_t xepoch, int c,
+                                                   uint32_t chain, int64_t it, int b, int m) {
+    return pchol32_impl<false>(d, mat, prow, pks, pos_out, NB, seed, xepoch, c, chain, it, b, m);
+  }
+#endif
+  template <bool OPT>
+  __device__ __forceinline__ static int pchol32_impl(int d, double* mat, double* prow, int* pks, int* pos_out,
+                                                     const DBlock* NB, uint64_t seed, int64_t xepoch, int c,
+                                                     uint32_t chain, int64_t it, int b, int m) {
+    const Grp<G> g;
     constexpr int RI = DMAX;  // prow[RI]: the pivot's reciprocal
     const int lane = g.lane;
     const bool hi_half = (threadIdx.x & 32) != 0;
@@ -397,6 +412,203 @@ struct Smp {
     int rank = d;
     int pe = 0;  // this lane's pivot position
     bool live = true;
+#ifndef MMB_PCHOL_V1
+    // Two passes over the same Sigma (mat is only read until the write-back):
+    // * the optimistic pass takes, per chain, the lane whose candidate dl = diag0 - work has
+    //   the largest int32 high word (the lowest such lane on a tie) as the pivot and stops
+    //   when every candidate is negative.  It never branches on the pivot search; it only
+    //   accumulates, on the scalar unit, whether a step was outside what that rule decides
+    //   exactly: a high-word tie, a NaN or >= 2^700 candidate, or a maximum below 2^-700
+    //   (then the in-range square root / reciprocal of device.h would not be the IEEE ones);
+    // * only if so (rare), the whole factorization is redone by the checked pass: the same
+    //   steps, with dpstf2's exact choice (pivot_exact: first maximum in position order, its
+    //   rank test) and sqrt() / division wherever a step needs them.
+    // Both give dpstf2's pivots and bits.  A lane that is done (its row finished) or out of
+    // range carries work = +inf, so its candidate is -inf and its key negative with no
+    // per-step select.  The row update of lij is the !done select only; the dot product runs
+    // on every lane (a DPP source lane must be active).
+    if (!inb) work = __builtin_inf();
+    // LDS byte address of mat (32-bit local address space)
+    const uint32_t mat_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)mat;
+    int hmask = hi_half ? -1 : 0;
+    asm volatile("" : "+v"(hmask));  // keep it a VGPR (not a scalar lane mask + select)
+    constexpr int KEY_LO = 0x14300000;     // high word of 2^-700
+    constexpr double BIG = 0x1p700;
+    // CHECKED: template constant (two inlined copies of the pass) or, with MMB_PCHOL_ONECOPY,
+    // a wave-uniform run-time flag that one copy of the pass branches on per step
+    auto pass = [&](auto checked_c) -> bool {
+#ifdef MMB_PCHOL_ONECOPY
+      const bool CHECKED = checked_c;
+#else
+      constexpr bool CHECKED = decltype(checked_c)::value;
+#endif
+      uint64_t needm = 0;  // wave-uniform: nonzero if a step of this pass was not decided exactly
+#pragma unroll
+      for (int j = 0; j < DMAX; ++j) {
+        if (live && j < d) {
+          const double dl = diag0 - work;
+          const int key = (int)(mmb_d2u(dl) >> 32);
+          const int mx = gmax_i32(key);
+          const uint64_t eq = __ballot(key == mx);
+          uint32_t elo = (uint32_t)eq, ehi = (uint32_t)(eq >> 32);
+          int p = 0;
+          bool pos = mx >= 0;  // dpstf2's ajj <= 0 stop: every candidate negative
+          bool fast = true;
+#ifdef MMB_PCHOL_ONECOPY
+          {
+            const int plo = __builtin_ctz(elo | 0x80000000u), phi = __builtin_ctz(ehi | 0x80000000u);
+            p = plo ^ ((plo ^ phi) & hmask);
+          }
+          if (CHECKED) {
+#else
+          if constexpr (!CHECKED) {
+            // p = plo in the lower chain, phi in the upper one, as plo ^ ((plo ^ phi) & hmask)
+            const int plo = __builtin_ctz(elo | 0x80000000u), phi = __builtin_ctz(ehi | 0x80000000u);
+            p = plo ^ ((plo ^ phi) & hmask);
+          } else {
+#endif
+            const uint64_t act = __builtin_amdgcn_read_exec();
+            const uint64_t bad = __ballot(!(dl < BIG));      // NaN, +inf or >= 2^700
+            const uint64_t big = __ballot(key >= KEY_LO);    // candidates >= 2^-700
+            const uint64_t neg = __ballot(mx < 0);
+            // per chain (32-bit half): inactive, or stopping, or a unique maximum >= 2^-700
+            uint32_t alo = (uint32_t)act, ahi = (uint32_t)(act >> 32);
+            uint32_t nlo = (uint32_t)neg, nhi = (uint32_t)(neg >> 32), blo = (uint32_t)big, bhi = (uint32_t)(big >> 32);
+            asm("" : "+s"(elo), "+s"(ehi), "+s"(alo), "+s"(ahi));
+            asm("" : "+s"(nlo), "+s"(nhi), "+s"(blo), "+s"(bhi));
+            const bool ok_lo = alo == 0 || nlo != 0 || ((elo & (elo - 1)) == 0 && blo != 0);
+            const bool ok_hi = ahi == 0 || nhi != 0 || ((ehi & (ehi - 1)) == 0 && bhi != 0);
+            fast = bad == 0 && ok_lo && ok_hi;
+            if (fast) {
+              const int plo = __builtin_ctz(elo | 0x80000000u), phi = __builtin_ctz(ehi | 0x80000000u);
+              p = plo ^ ((plo ^ phi) & hmask);
+            } else {
+              double val;
+              p = pivot_exact(dl, done, pks, j, d, (int*)prow, &val);
+              pos = val > 0.0;
+            }
+          }
+          if (!pos) {
+            live = false;  // rank = pivots taken, counted after the loop
+          } else {
+            const bool piv = lane == p;
+            if (piv) {
+              pks[j] = p;
+              if (j + 1 < d) {  // the last step has no rows left to update: no readers
+#pragma unroll
+                for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
+                if (j & 1) prow[j - 1] = Lrow[j - 1];
+              }
+              double ajj, rinv;
+              if (fast) {
+                mmb_sqrt_rcp_inrange(dl, &ajj, &rinv);  // IEEE results in the fast range (device.h)
+              } else {
+                ajj = sqrt(dl);
+                rinv = 1.0 / ajj;
+              }
+              prow[RI] = rinv;
+              Lrow[j] = ajj;
+              pe = j;
+              work = __builtin_inf();
+              done = true;
+            }
+            grp_sync();
+            if (j + 1 < d) {  // (j = d - 1: every lane is done)
+              // pivot row: lane l of each 16-lane row reads elements l and 16 + l, then every
+              // product takes element k from lane k % 16 of its row by a DPP64 row_newbcast operand
+              double t0 = 0.0, t1 = 0.0;
+              // Sigma(lc, p) at byte 8 slot = 4 a (a + 1) + 8 b, a = max, b = min
+              const int sa = max(lc, p), sb = min(lc, p);
+              int sq, ad;  // sa (sa + 1) in one instruction; byte address by two shift-adds
+              asm("v_mad_u32_u24 %0, %1, %1, %1" : "=v"(sq) : "v"(sa));
+              asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(ad) : "v"(sb), "v"(mat_lds));
+              asm("v_lshl_add_u32 %0, %1, 2, %0" : "+v"(ad) : "v"(sq));
+              double sig = *(const __attribute__((address_space(3))) double*)(uintptr_t)(uint32_t)ad;
+              double rinv = prow[RI];
+              double pA = prow[lane & 15];
+              double pB = j > 16 ? prow[16 + (lane & 15)] : 0.0;
+              asm volatile("" : "+v"(sig), "+v"(rinv), "+v"(pA));
+              if (j > 16) asm volatile("" : "+v"(pB));
+              if (j > 0) {
+#pragma unroll
+                for (int k = 0; k < j; ++k) {
+                  const double src = k < 16 ? pA : pB;
+                  if (k & 1) fmac_rowbc_n(t1, src, Lrow[k], k & 15);
+                  else fmac_rowbc_n(t0, src, Lrow[k], k & 15);
+                }
+              }
+              const double lij = (sig - (t0 + t1)) * rinv;
+              // done lanes carry work = +inf, which absorbs lij^2: no select for work
+              work = work + lij * lij;
+              if (!done) Lrow[j] = lij;
+            }
+            grp_sync();
+          }
+#ifndef MMB_PCHOL_ONECOPY
+          if constexpr (!CHECKED)
+#endif
+          {
+            // scalar bookkeeping off the step's dependency chain (after the row update, no
+            // branch): ties of a chain that takes a pivot, NaN / huge candidates, tiny maxima
+#ifdef MMB_EXP_SCHEDB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            const uint64_t bad = __ballot(!(dl < BIG));                     // NaN, +inf, >= 2^700
+            const uint64_t tiny = __ballot((uint32_t)mx < (uint32_t)KEY_LO);  // 0 <= max < 2^-700
+            const uint64_t neg = __ballot(mx < 0);
+            uint32_t nlo = (uint32_t)neg, nhi = (uint32_t)(neg >> 32);
+            asm("" : "+s"(elo), "+s"(ehi), "+s"(nlo), "+s"(nhi));
+            // (a stopping chain's -inf keys tie: ignored)
+            const uint32_t tie = ((elo & (elo - 1)) & (nlo ? 0u : ~0u)) | ((ehi & (ehi - 1)) & (nhi ? 0u : ~0u));
+            needm |= bad | tiny | (uint64_t)tie;
+          }
+        }
+      }
+      return needm != 0;
+    };
+#if defined(MMB_PCHOL_ONECOPY)
+    // one copy of the pass, run once optimistically and, rarely, again checked
+#pragma nounroll
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      int ck = attempt;
+      asm volatile("" : "+s"(ck));  // opaque: no peeled second copy
+      if (ck) {  // rare: redo with dpstf2's exact decisions
+        work = inb ? 0.0 : __builtin_inf();
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
+        done = !inb;
+        pe = 0;
+        live = true;
+      }
+      if (!pass(ck != 0) || ck) break;
+    }
+#else
+    if constexpr (OPT) {
+#if defined(MMB_EXP_FORCEFAST) || defined(MMB_EXP_NOREDO)
+      (void)pass(std::false_type{});  // timing experiments only: the optimistic pass alone
+#elif defined(MMB_PCHOL_EXACT_NOINLINE)
+      if (pass(std::false_type{}))    // rare: redo with dpstf2's exact decisions, out of line
+        return pchol32_exact(d, mat, prow, pks, pos_out, NB, seed, xepoch, c, chain, it, b, m);
+#else
+      if (pass(std::false_type{})) {  // rare: redo with dpstf2's exact decisions
+        work = inb ? 0.0 : __builtin_inf();
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
+        done = !inb;
+        pe = 0;
+        live = true;
+        (void)pass(std::true_type{});
+      }
+#endif
+    } else {
+      (void)pass(std::true_type{});
+    }
+#endif
+    {
+      const uint64_t dn = __ballot(done && inb);
+      rank = __builtin_popcount(hi_half ? (uint32_t)(dn >> 32) : (uint32_t)dn);
+    }
+#else
 #pragma unroll
     for (int j = 0; j < DMAX; ++j) {
       if (live && j < d) {
@@ -500,11 +712,12 @@ struct Smp {
         }
       }
     }
+#endif  // MMB_PCHOL_V1
     MMB_PROF_MARK(10, lane)
     // carried proposal of the next iteration (see amm): formed here, where the factor rows are
     // still in registers; skipped when the next proposal would need an older factor
     if (NB != nullptr && (rank == d || m <= 2 * d)) {
-      const mmb_rng rn1 = mmb_rng_make(A.seed, chain, (uint32_t)(it + 1), (uint32_t)b, MMB_SUB_NORMAL);
+      const mmb_rng rn1 = mmb_rng_make(seed, chain, (uint32_t)(it + 1), (uint32_t)b, MMB_SUB_NORMAL);
       double z1n = 0.0, z2n = 0.0;
       if (inb) mmb_normal_pair(&rn1, (uint32_t)lane, &z1n, &z2n);
       double a = 0.0;
@@ -534,7 +747,7 @@ struct Smp {
         a = NB->beta * a + (1.0 - NB->beta) * y;
       }
       if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
-      if (lane == 0) NB->t_xtag[c] = xtag(A, it + 1);
+      if (lane == 0) NB->t_xtag[c] = (xepoch << 32) | (int64_t)(uint32_t)(it + 1);  // xtag()
     }
     MMB_PROF_MARK(11, lane)
     if (rank == d && inb) {  // the factor in position form: row at position pe at tri(pe) + k

@@ -202,3 +202,64 @@ def test_julia_chains_rows_equal_kept_count():
         rows = len(range(burnin + thin, last + 1, thin))
         kept = sum(1 for i in range(first, last + 1) if i > burnin and (i - burnin) % thin == 0)
         assert rows == kept, (first, last, burnin, thin)
+
+
+def _julia_fields(src, name):
+    m = re.search(rf"^immutable {name}\b(.*?)^end", src, re.M | re.S)
+    assert m, name
+    body = re.sub(r"#.*", "", m.group(1))
+    return re.findall(r"(\w+)::([\w{},]+)", body)
+
+
+def _c_fields(name):
+    txt = open(HDR).read()
+    m = re.search(r"typedef struct \{([^{}]*)\}\s*" + name + ";", txt)
+    assert m, name
+    body = re.sub(r"/\*.*?\*/", "", m.group(1), flags=re.S)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        typ, names = re.match(r"((?:const\s+)?\w+\s*\**)\s*(.*)", decl).groups()
+        for nm in names.split(","):
+            nm = nm.strip()
+            star = nm.count("*") + typ.count("*")
+            nm = nm.strip("* ")
+            arr = re.match(r"(\w+)\[(\w+)\]", nm)
+            out.append((arr.group(1) if arr else nm, typ.replace("const", "").strip(" *"), star,
+                        arr.group(2) if arr else None))
+    return out
+
+
+JL_C = {"Int32": "int32_t", "Int64": "int64_t", "Float64": "double", "IrBlock": "mmb_ir_block"}
+
+
+@pytest.mark.parametrize("jl,c", [("IrNode", "mmb_ir_node"), ("IrBlock", "mmb_ir_block"),
+                                  ("IrModel", "mmb_ir_model"), ("BlockSpec", "mmb_block_spec")])
+def test_julia_structs_match_header(jl, c):
+    """The Julia shim's immutable structs (ccall'd by reference) have the header's fields in
+    the header's order with the same C types: the node-IR lowering (lower_ir ->
+    mmb_create_ir) and the block specs reach the library with the right layout."""
+    jf, cf = _julia_fields(_julia_src(), jl), _c_fields(c)
+    arrays = {"MMB_IR_MAX_TERMS": 16, "MMB_MAX_BLOCKS": 8, "MMB_MAX_NODES_PER_BLOCK": 4}
+    assert [n for n, _ in jf] == [n for n, *_ in cf], (jf, cf)
+    for (jn, jt), (cn, ct, star, arr) in zip(jf, cf):
+        if star:
+            assert jt.startswith("Ptr{"), (jn, jt, ct)
+        elif arr:
+            n = arrays.get(arr, int(arr) if arr.isdigit() else None)
+            inner = re.match(r"NTuple\{(\d+),(\w+)\}", jt)
+            assert inner and int(inner.group(1)) == n, (jn, jt, arr)
+            assert JL_C.get(inner.group(2)) == ct, (jn, jt, ct)
+        else:
+            assert JL_C.get(jt) == ct, (jn, jt, ct)
+
+
+def test_julia_ir_lowering_present():
+    """the shim lowers any other DAG to the node IR through the reference's
+    own node functions (node.eval on a tracer Model) and term lists (keys(m, :target, b))."""
+    code = "\n".join(l.split("#")[0] for l in _julia_src().splitlines())
+    for needle in ["function lower_ir_(m::Model)", "node.eval(tm)", "m[k].eval(tm)", "keys(m, :target, b)",
+                   "keys(m, :dependent)", "ccall((:mmb_create_ir, libmambahip)", "irl = lower_ir(m)"]:
+        assert needle in code, needle

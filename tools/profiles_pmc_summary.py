@@ -68,6 +68,22 @@ if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
                "scheme": a.scheme, "chains": cfg.get("chains_per_gpu"), "iters_per_launch": cfg.get("iters_per_launch"),
                "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()},
               open(a.prefix + "_hbm_traffic.json", "w"), indent=1)
+# FP64 VALU lane-flops (the reference Slice+AMWG scheme is bound by them, SURVEY §8(d) row 3'):
+# the SQ_INSTS_VALU_*_F64 counters count wave instructions; x 64 lanes, an FMA = 2 flops
+f64 = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"]
+if all(k in out for k in f64) and os.path.exists(bench):
+    fl = 64.0 * (out[f64[0]] + out[f64[1]] + 2.0 * out[f64[2]] + out[f64[3]])
+    upd = b["roofline"]["chain_updates_per_launch"]
+    out["f64_lane_flops_per_launch"] = fl
+    out["f64_lane_flops_per_chain_update"] = fl / upd
+    cfg = b["config"]
+    json.dump({"f64_lane_flops_per_chain_update": fl / upd, "f64_lane_flops_per_launch": fl,
+               "source": os.path.basename(a.prefix) + "_sweep_summary.json",
+               "formula": "64 * (ADD_F64 + MUL_F64 + 2 * FMA_F64 + TRANS_F64) wave instructions per launch "
+                          "(SQ_INSTS_VALU_*_F64), / chain-updates per launch; last %d launches" % a.last,
+               "scheme": a.scheme, "chains": cfg.get("chains_per_gpu"), "iters_per_launch": cfg.get("iters_per_launch"),
+               "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest()},
+              open(a.prefix + "_valu_flops.json", "w"), indent=1)
 if os.path.exists(st):
     shutil.copy(st, a.prefix + "_kernel_stats.csv")
 json.dump(out, open(a.prefix + "_sweep_summary.json", "w"), indent=1)

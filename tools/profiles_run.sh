@@ -5,8 +5,8 @@ set -e
 OUT=${1:-gpurun_out/prof}
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--steps 200 --warmup 200 --no-cpu-baseline"
-timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+ARGS="--steps 200 --warmup 200 --no-cpu-baseline $BENCH_EXTRA"  # BENCH_EXTRA e.g. "--scheme reference"
+timeout -k 10 600 python bench.py $BENCH_EXTRA > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py $ARGS > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py $ARGS > $OUT/pmc_write.log 2>&1
