@@ -360,6 +360,73 @@ struct Smp {
     return max((int)r[0], (int)r[1]);
   }
 
+  // The checked factorization as a compact loop (not unrolled; the row lives in a private
+  // array): the rare redo after an optimistic pass of pchol32 that met a tie, a NaN or a
+  // maximum outside the in-range square root's domain.  dpstf2's pivot (pivot_exact: first
+  // maximum in position order, NaN semantics) and its ajj <= 0 stop, IEEE sqrt() and 1.0 / x,
+  // and the same two-accumulator dot product (even / odd k) as the unrolled steps, so the
+  // factor is bit-identical to what the checked unrolled pass computes.  Leaves the rows in
+  // Lrow[], the positions in pe, done / work as the unrolled pass does.
+#ifdef MMB_REDO_INLINE
+  __device__ __forceinline__
+#else
+  __device__ __attribute__((noinline))
+#endif
+  static void redo_exact_impl(int d, double* mat, double* prow, int* pks,
+                                                                    double diag0, int lc, bool inb, double* Lx,
+                                                                    double* work_, bool* done_, int* pe_) {
+    const int lane = (int)(threadIdx.x & (G - 1));
+    double work = inb ? 0.0 : __builtin_inf();
+    bool done = !inb, live = true;
+    int pe = 0;
+    for (int k = 0; k < DMAX; ++k) Lx[k] = 0.0;
+#pragma nounroll
+    for (int j = 0; j < d; ++j) {
+      if (live) {
+        const double dl = diag0 - work;
+        double val;
+        const int p = pivot_exact(dl, done, pks, j, d, (int*)prow, &val);
+        if (!(val > 0.0)) {
+          live = false;
+        } else {
+          if (lane == p) {
+            pks[j] = p;
+            for (int k = 0; k < j; ++k) prow[k] = Lx[k];
+            const double ajj = sqrt(dl);
+            prow[DMAX] = 1.0 / ajj;
+            Lx[j] = ajj;
+            pe = j;
+            work = __builtin_inf();
+            done = true;
+          }
+          grp_sync();
+          if (j + 1 < d) {
+            double t0 = 0.0, t1 = 0.0;
+            for (int k = 0; k < j; ++k) {
+              if (k & 1) t1 = fma(prow[k], Lx[k], t1);
+              else t0 = fma(prow[k], Lx[k], t0);
+            }
+            const double lij = (mat[mmb_slot(lc, p)] - (t0 + t1)) * prow[DMAX];
+            work = work + lij * lij;
+            if (!done) Lx[j] = lij;
+          }
+          grp_sync();
+        }
+      }
+    }
+    *work_ = work;
+    *done_ = done;
+    *pe_ = pe;
+  }
+  __device__ __forceinline__ static void redo_exact(int d, double* mat, double* prow, int* pks, double diag0,
+                                                    int lc, bool inb, double (&Lrow)[DMAX], double& work,
+                                                    bool& done, int& pe) {
+    double Lx[DMAX];
+    redo_exact_impl(d, mat, prow, pks, diag0, lc, inb, Lx, &work, &done, &pe);
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) Lrow[k] = Lx[k];
+  }
+
   // pchol for 32-lane groups with one row per lane (rats), same results as pchol():
   // * the pivot lane computes sqrt / reciprocal of its remaining diagonal by the in-range
   //   sequences of device.h (bit-identical to sqrt() and 1.0 / x there) and publishes the
@@ -412,6 +479,59 @@ struct Smp {
     int rank = d;
     int pe = 0;  // this lane's pivot position
     bool live = true;
+    // the factorization's epilogue (carried proposal, write-back)
+    auto tail = [&]() __attribute__((always_inline)) -> int {
+      MMB_PROF_MARK(10, lane)
+      // carried proposal of the next iteration (see amm): formed here, where the factor rows are
+      // still in registers; skipped when the next proposal would need an older factor
+      if (NB != nullptr && (rank == d || m <= 2 * d)) {
+        const mmb_rng rn1 = mmb_rng_make(seed, chain, (uint32_t)(it + 1), (uint32_t)b, MMB_SUB_NORMAL);
+        double z1n = 0.0, z2n = 0.0;
+        if (inb) mmb_normal_pair(&rn1, (uint32_t)lane, &z1n, &z2n);
+        double a = 0.0;
+        if (inb) a = fma(NB->sigl[lane * d + lane], z1n, a);
+        if (m > 2 * d) {
+          // rows are zero past the lane's own step, so the full sweep adds exact zeros
+          double y = 0.0;
+#ifdef MMB_EXP_LDS_CARRY
+          prow[lane] = z2n;
+          grp_sync();
+#pragma unroll
+          for (int k = 0; k < DMAX; k += 2) {
+            const double2 zz = *(const double2*)(prow + k);
+            y = fma(Lrow[k], zz.x, y);
+            if (k + 1 < DMAX) y = fma(Lrow[k + 1], zz.y, y);
+          }
+          grp_sync();
+#else
+          // z2'[k] lives in lane k: rows 0 / 1 of the group exchange theirs (permlane16 swap),
+          // then each product takes z2'[k] from lane k % 16 of the row (DPP64 row_newbcast)
+          const double zs = swap16_d(z2n);
+          const bool row0 = (lane & 16) == 0;
+          const double zA = row0 ? z2n : zs, zB = row0 ? zs : z2n;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) fmac_rowbc_n(y, k < 16 ? zA : zB, Lrow[k], k & 15);
+#endif
+          a = NB->beta * a + (1.0 - NB->beta) * y;
+        }
+        if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
+        if (lane == 0) NB->t_xtag[c] = (xepoch << 32) | (int64_t)(uint32_t)(it + 1);  // xtag()
+      }
+      MMB_PROF_MARK(11, lane)
+      if (rank == d && inb) {  // the factor in position form: row at position pe at tri(pe) + k
+        // one store per k from every lane, no exec-mask change: entries past the row's end
+        // (k > pe, exact zeros) go to the lane's own dummy slot in the idle pivot-row buffer
+        const int base = mmb_tri(pe);
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          double* dst = k <= pe ? mat + base + k : prow + lane;
+          *dst = Lrow[k];
+        }
+      }
+      MMB_PROF_MARK(12, lane)
+      *pos_out = pe;
+      return rank;
+    };
 #ifndef MMB_PCHOL_V1
     // Two passes over the same Sigma (mat is only read until the write-back):
     // * the optimistic pass takes, per chain, the lane whose candidate dl = diag0 - work has
@@ -436,7 +556,7 @@ struct Smp {
     constexpr double BIG = 0x1p700;
     // CHECKED: template constant (two inlined copies of the pass) or, with MMB_PCHOL_ONECOPY,
     // a wave-uniform run-time flag that one copy of the pass branches on per step
-    auto pass = [&](auto checked_c) -> bool {
+    auto pass = [&](auto checked_c) __attribute__((always_inline)) -> bool {
 #ifdef MMB_PCHOL_ONECOPY
       const bool CHECKED = checked_c;
 #else
@@ -447,6 +567,15 @@ struct Smp {
       for (int j = 0; j < DMAX; ++j) {
         if (live && j < d) {
           const double dl = diag0 - work;
+#ifdef MMB_EXP_HOIST
+          // every lane's square root and reciprocal, independent of the search: the two
+          // dependency chains interleave (the pivot lane then publishes at once)
+          double ajj_h = 0.0, rinv_h = 0.0;
+          if (!CHECKED) {
+            mmb_sqrt_rcp_inrange(dl, &ajj_h, &rinv_h);
+            asm volatile("" : "+v"(ajj_h), "+v"(rinv_h));
+          }
+#endif
           const int key = (int)(mmb_d2u(dl) >> 32);
           const int mx = gmax_i32(key);
           const uint64_t eq = __ballot(key == mx);
@@ -501,6 +630,12 @@ struct Smp {
               }
               double ajj, rinv;
               if (fast) {
+#ifdef MMB_EXP_HOIST
+                if (!CHECKED) {
+                  ajj = ajj_h;
+                  rinv = rinv_h;
+                } else
+#endif
                 mmb_sqrt_rcp_inrange(dl, &ajj, &rinv);  // IEEE results in the fast range (device.h)
               } else {
                 ajj = sqrt(dl);
@@ -589,8 +724,14 @@ struct Smp {
 #elif defined(MMB_PCHOL_EXACT_NOINLINE)
       if (pass(std::false_type{}))    // rare: redo with dpstf2's exact decisions, out of line
         return pchol32_exact(d, mat, prow, pks, pos_out, NB, seed, xepoch, c, chain, it, b, m);
+#elif defined(MMB_PCHOL_COMPACT_REDO)
+      if (pass(std::false_type{})) {  // rare: redo with dpstf2's exact decisions, compact loop
+        redo_exact(d, mat, prow, pks, diag0, lc, inb, Lrow, work, done, pe);
+      }
 #else
-      if (pass(std::false_type{})) {  // rare: redo with dpstf2's exact decisions
+      // rare (a few per thousand factorizations): redo with dpstf2's exact decisions; marked
+      // unlikely so the block placement moves the checked pass out of the hot code
+      if (__builtin_expect(pass(std::false_type{}), 0)) {
         work = inb ? 0.0 : __builtin_inf();
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
@@ -713,56 +854,7 @@ struct Smp {
       }
     }
 #endif  // MMB_PCHOL_V1
-    MMB_PROF_MARK(10, lane)
-    // carried proposal of the next iteration (see amm): formed here, where the factor rows are
-    // still in registers; skipped when the next proposal would need an older factor
-    if (NB != nullptr && (rank == d || m <= 2 * d)) {
-      const mmb_rng rn1 = mmb_rng_make(seed, chain, (uint32_t)(it + 1), (uint32_t)b, MMB_SUB_NORMAL);
-      double z1n = 0.0, z2n = 0.0;
-      if (inb) mmb_normal_pair(&rn1, (uint32_t)lane, &z1n, &z2n);
-      double a = 0.0;
-      if (inb) a = fma(NB->sigl[lane * d + lane], z1n, a);
-      if (m > 2 * d) {
-        // rows are zero past the lane's own step, so the full sweep adds exact zeros
-        double y = 0.0;
-#ifdef MMB_EXP_LDS_CARRY
-        prow[lane] = z2n;
-        grp_sync();
-#pragma unroll
-        for (int k = 0; k < DMAX; k += 2) {
-          const double2 zz = *(const double2*)(prow + k);
-          y = fma(Lrow[k], zz.x, y);
-          if (k + 1 < DMAX) y = fma(Lrow[k + 1], zz.y, y);
-        }
-        grp_sync();
-#else
-        // z2'[k] lives in lane k: rows 0 / 1 of the group exchange theirs (permlane16 swap),
-        // then each product takes z2'[k] from lane k % 16 of the row (DPP64 row_newbcast)
-        const double zs = swap16_d(z2n);
-        const bool row0 = (lane & 16) == 0;
-        const double zA = row0 ? z2n : zs, zB = row0 ? zs : z2n;
-#pragma unroll
-        for (int k = 0; k < DMAX; ++k) fmac_rowbc_n(y, k < 16 ? zA : zB, Lrow[k], k & 15);
-#endif
-        a = NB->beta * a + (1.0 - NB->beta) * y;
-      }
-      if (inb) NB->t_xnext[(size_t)c * DP + lane] = a;
-      if (lane == 0) NB->t_xtag[c] = (xepoch << 32) | (int64_t)(uint32_t)(it + 1);  // xtag()
-    }
-    MMB_PROF_MARK(11, lane)
-    if (rank == d && inb) {  // the factor in position form: row at position pe at tri(pe) + k
-      // one store per k from every lane, no exec-mask change: entries past the row's end
-      // (k > pe, exact zeros) go to the lane's own dummy slot in the idle pivot-row buffer
-      const int base = mmb_tri(pe);
-#pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        double* dst = k <= pe ? mat + base + k : prow + lane;
-        *dst = Lrow[k];
-      }
-    }
-    MMB_PROF_MARK(12, lane)
-    *pos_out = pe;
-    return rank;
+    return tail();
   }
 
   // (i, k) of every packed slot, i << 8 | k, one table per workgroup in LDS (filled once per
@@ -985,26 +1077,38 @@ struct Smp {
         }
       }
       grp_sync();
-      // the lane's own Mvv slots straight into registers, all loads in flight at once
+      // the lane's own Mvv slots straight into registers, all loads in flight at once.  Slots
+      // T <= t < TP are the row's padding (never read as Mvv / Sigma): they are updated like the
+      // others from stale scratch, so no slot needs a branch (rats: NT * G == TP exactly), and
+      // the new values are stored after the slot loop -- an HBM store between two uses of the
+      // loaded values would make every use wait for the stores before it (vmcnt(0)).
       double lt[NT];
 #pragma unroll
-      for (int u = 0; u < NT; ++u) lt[u] = (!fresh && u * G + g.lane < T) ? Mvv[u * G + g.lane] : 0.0;
+      for (int u = 0; u < NT; ++u) lt[u] = (!fresh && u * G + g.lane < TP) ? Mvv[u * G + g.lane] : 0.0;
       // slot t = u G + lane: HBM and LDS addresses are the lane's base + a constant per u
       // (immediate offsets), the fresh / steady choice is made once outside the slot loop
       double* const Mvv_l = Mvv + g.lane;
       double* const mat_l = mat + g.lane;
       auto slots = [&](auto fresh_c) {
         constexpr bool FRESH = decltype(fresh_c)::value;
+#ifndef MMB_EXP_IK_PERSLOT
+        // opaque once per update: the table reads can be issued together (one LDS wait), but
+        // not hoisted out of the iteration loop (2 * NT ints live across it: spills)
+        int li0 = g.lane;
+        asm volatile("" : "+v"(li0));
+#endif
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           const int t = u * G + g.lane;
-          if (t < T) {
-            // opaque to the optimiser: decoding (i, k) here is a few VALU ops, while hoisting
-            // all NT pairs out of the iteration loop keeps 2*NT ints live (spills)
+          if ((u + 1) * G <= TP || t < TP) {
             int i, k;
             if constexpr (IKTAB) {
+#ifdef MMB_EXP_IK_PERSLOT
               int li = g.lane;
               asm volatile("" : "+v"(li));
+#else
+              const int li = li0;
+#endif
               const int w = ik_table()[li + u * G];
               i = w >> 8;
               k = w & 255;
@@ -1016,13 +1120,16 @@ struct Smp {
             const double2 a = vm[k], bi = vm[i];
             const double old = FRESH ? z2s[i] * z2s[k] : lt[u];
             const double nv = p * old + (q * a.x) * bi.x;
-            Mvv_l[u * G] = nv;
+            lt[u] = nv;
             mat_l[u * G] = cc * (nv - a.y * bi.y);
           }
         }
       };
       if (fresh) slots(std::true_type{});
       else slots(std::false_type{});
+#pragma unroll
+      for (int u = 0; u < NT; ++u)
+        if ((u + 1) * G <= TP || u * G + g.lane < TP) Mvv_l[u * G] = lt[u];
       grp_sync();
       // everything but the factorization is finished first; the chain state is parked
       // in LDS so the Cholesky's register footprint does not stack on top of it
