@@ -422,6 +422,7 @@ def main():
         if args.workload == "rats":
             ref = rats_model(mb, scheme_for(mb, "reference"))
             out["cpu_baseline"] = cpu_baseline(model, init_all, args.cpu_seconds,
+                                               what=f"rats {args.scheme} sweep",
                                                extra=("reference_scheme", ref, init_all))
         elif args.workload == "line_amm":
             out["cpu_baseline"] = cpu_baseline(model, init_all, args.cpu_seconds, "line AMM update",
