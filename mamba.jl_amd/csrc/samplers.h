@@ -617,7 +617,16 @@ struct Smp {
               pos = val > 0.0;
             }
           }
-          if (!pos) {
+#ifdef MMB_PCHOL_STOPBR
+          constexpr bool NOBR = false;
+#else
+          // optimistic pass: no branch on the stop either -- a chain whose candidates are all
+          // negative runs this step on a garbage pivot (one of its done / out-of-range lanes,
+          // whose -inf keys are the largest negative ones) and stops after it; a stopped
+          // chain's factor is never used (rank < d) and its done set is unchanged
+          constexpr bool NOBR = !CHECKED;
+#endif
+          if (!NOBR && !pos) {
             live = false;  // rank = pivots taken, counted after the loop
           } else {
             const bool piv = lane == p;
@@ -678,6 +687,7 @@ struct Smp {
               if (!done) Lrow[j] = lij;
             }
             grp_sync();
+            if (NOBR) live = live && pos;
           }
 #ifndef MMB_PCHOL_ONECOPY
           if constexpr (!CHECKED)
@@ -748,6 +758,9 @@ struct Smp {
     {
       const uint64_t dn = __ballot(done && inb);
       rank = __builtin_popcount(hi_half ? (uint32_t)(dn >> 32) : (uint32_t)dn);
+      // (an optimistic stop at step 0 of a 32-element block has no done / out-of-range lane to
+      // take the garbage pivot: it marked one live lane)
+      if (!live && d == G && rank == 1) rank = 0;
     }
 #else
 #pragma unroll
