@@ -59,10 +59,14 @@ def parse():
     p.add_argument("--thin", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=20.0)
+    p.add_argument("--nuts-burnin", type=int, default=None,
+                   help="logistic: Model.burnin of the timed run (default steps // 2: 1000 of 2000)")
     p.add_argument("--scheme", default="gibbs_amm",
                    help="gibbs_amm (metric config) | reference | ablations: amm_noadapt, gibbs_only")
     a = p.parse_args()
-    dflt = {"rats": (CHAINS_PER_GPU, 400, 200), "line_amm": (4096, 2000, 500), "logistic": (4096, 100, 100),
+    # logistic (configs[3]): the timed steps are the config's whole run, 2000
+    # iterations with NUTS adapting for the first 1000 (--nuts-burnin), on re-initialised chains
+    dflt = {"rats": (CHAINS_PER_GPU, 400, 200), "line_amm": (4096, 2000, 500), "logistic": (4096, 2000, 20),
             "seeds_ir": (CHAINS_PER_GPU, 160, 80), "rats_ir": (CHAINS_PER_GPU, 64, 32)}
     k, st, wu = dflt[a.workload]
     a.chains = a.chains or k
@@ -278,11 +282,18 @@ def main():
     # then the device draw buffer for the timed window's kept rows: no allocation in the window
     eng.run(args.warmup, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False,
             time_kernels=True)
+    tburn = pre + args.warmup
+    if nuts:
+        # the config's own run: fresh chains, NUTS adapting while iter <= nuts_burnin (nuts.jl:52),
+        # kept draws after it (mcmc(m, ..., 2000, burnin=1000)); the warm-up above only warmed
+        # the kernels and the engine's buffers
+        eng.init_chains(init_all, chain_offset=rank * K, seed=20261015)
+        mburn = tburn = args.nuts_burnin if args.nuts_burnin is not None else args.steps // 2
     eng.reserve_draws(args.steps // thin + 1)
     nuts_before = eng.nuts_stats() if nuts else None
     barrier()
     t0 = time.perf_counter()
-    eng.run(args.steps, burnin=pre + args.warmup, thin=thin, model_burnin=mburn, draws=False, keep_device=True,
+    eng.run(args.steps, burnin=tburn, thin=thin, model_burnin=mburn, draws=False, keep_device=True,
             time_kernels=True)
     barrier()
     dt = time.perf_counter() - t0
@@ -298,7 +309,7 @@ def main():
     if kernel_ms_per_step > 1.05 * ms_per_step:
         raise SystemExit(f"bench: kernel time per step {kernel_ms_per_step:.4f} ms exceeds the timed "
                          f"window's {ms_per_step:.4f} ms by more than 5 % — timing is inconsistent")
-    grads_timed = eng.grad_evals() if nuts else 0
+    grads_timed = eng.grad_evals() if nuts else 0  # (the counter restarts with every mmb_run)
     nuts_timed = None
     if nuts:
         after = eng.nuts_stats()
@@ -344,16 +355,17 @@ def main():
     # roofline of the dominant kernel; per-launch device time from HIP events on the engine's
     # stream, over full launches in the same steady state as the timed window
     if nuts:  # lg_grad_kernel: 4*N*p algorithmic flops per gradient (X*beta and X'*res)
-        nroof = 16
-        eng.run(nroof, burnin=0, thin=1, model_burnin=mburn, draws=False, time_kernels=True)
-        kms, launches, units = eng.kernel_time()
-        flops = 4.0 * 10000 * 50 * eng.grad_evals()
+        # measured over the timed window itself (the config's whole 2000-iteration run): its
+        # gradient count and the HIP-event time of its gradient launches
+        kms, launches = t_kms, t_launches
+        flops = 4.0 * 10000 * 50 * grads_timed
         achieved = flops / (kms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None,
                 "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": 4.0 * 10000 * 50,
-                "avg_launch_ms": kms / launches, "gradients_per_launch": eng.grad_evals() / launches,
-                "gradients_per_chain_update_timed": grads_timed / (K * args.steps)}
+                "avg_launch_ms": kms / launches, "gradients_per_launch": grads_timed / launches,
+                "gradients_per_chain_update_timed": grads_timed / (K * args.steps),
+                "window": f"timed run: {args.steps} iterations, burnin {tburn}"}
     else:
         W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
                                "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "64"))
