@@ -83,3 +83,18 @@ def test_dpp_sources_have_wait_states(tmp_path):
                     last_write[r] = i
         ws_at.append(ws_at[-1] + cost)
     assert checked > 100, checked   # the rats / node-IR factorization steps are covered
+
+
+def test_isa_census_finds_the_factorization_steps():
+    """tools/isa_census.py locates the 30 steps of the rats factorization (step j: j DPP fmacs)."""
+    if not os.path.exists(OBJ) or not os.path.exists(os.path.join(LLVM, "llvm-objdump")):
+        pytest.skip("no in-tree build object or ROCm LLVM tools")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_census", os.path.join(ROOT, "tools", "isa_census.py"))
+    ic = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ic)
+    ins = ic.kernel_instructions(ic.disassemble())
+    steps = ic.factorization_steps(ins)
+    assert len(steps) == 30
+    for j, (lo, hi) in enumerate(steps):
+        assert sum(1 for mn, _ in ins[lo:hi] if mn == "v_fmac_f64_dpp") == j
