@@ -308,7 +308,8 @@ int mmb_state_bytes(const mmb_engine* e, double* bytes_per_chain_update);
  * summed over chains; counted on device by the batched-gradient (logistic) engine, 0 else. */
 int mmb_grad_evals(mmb_engine* e, int64_t* n);
 /* NUTS tree statistics since mmb_init_chains, all NUTS blocks and chains: out[0] = completed
- * updates, out[1] = updates stopped by the depth cap MMB_NUTS_MAX_DEPTH (16) while the
+ * updates, out[1] = updates stopped by the depth cap MMB_NUTS_MAX_DEPTH (30: 2^30 leapfrogs
+ * in one update, beyond any run that finishes) while the
  * reference's unbounded doubling loop (nuts.jl:106-125) would have continued, out[2] = sum of
  * final tree depths j.  out[1] == 0 means the cap never changed a draw. */
 int mmb_nuts_stats(mmb_engine* e, int64_t out[3]);

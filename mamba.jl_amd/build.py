@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "lib", "libmambahip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-SOURCES = ["sweep.hip", "gr.hip", "logistic.hip", "summary.hip", "engine.cpp"]
+SOURCES = ["sweep.hip", "line_amm.hip", "gr.hip", "logistic.hip", "summary.hip", "engine.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-mllvm", "-pragma-unroll-threshold=100000",  # pchol32's 30 steps stay fully unrolled
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]

@@ -184,6 +184,26 @@ __device__ __forceinline__ void fmac_rowbc_n(double& acc, double x, double b, in
   }
 }
 
+// as fmac_rowbc_n with the first use of the source at an explicit step (a dot product whose
+// first products are formed otherwise)
+__device__ __forceinline__ void fmac_rowbc_nf(double& acc, double x, double b, int n, bool first) {
+  if (first) {
+    switch (n) {
+#define MMB_RBC(i) case i: fmac_rowbc<i, true>(acc, x, b); break;
+      MMB_RBC(0) MMB_RBC(1) MMB_RBC(2) MMB_RBC(3) MMB_RBC(4) MMB_RBC(5) MMB_RBC(6) MMB_RBC(7)
+      MMB_RBC(8) MMB_RBC(9) MMB_RBC(10) MMB_RBC(11) MMB_RBC(12) MMB_RBC(13) MMB_RBC(14) MMB_RBC(15)
+#undef MMB_RBC
+    }
+  } else {
+    switch (n) {
+#define MMB_RBC(i) case i: fmac_rowbc<i, false>(acc, x, b); break;
+      MMB_RBC(0) MMB_RBC(1) MMB_RBC(2) MMB_RBC(3) MMB_RBC(4) MMB_RBC(5) MMB_RBC(6) MMB_RBC(7)
+      MMB_RBC(8) MMB_RBC(9) MMB_RBC(10) MMB_RBC(11) MMB_RBC(12) MMB_RBC(13) MMB_RBC(14) MMB_RBC(15)
+#undef MMB_RBC
+    }
+  }
+}
+
 // stage s of the 32-lane all-reduce: partner lanes xor1, xor2 (quad_perm), 7-i (row_half_mirror),
 // 15-i (row_mirror), i^16 (permlane16_swap).  After stage s every lane of the 2^(s+1) subgroup
 // holds the same (commutative) combination.

@@ -257,15 +257,19 @@ MMB_HD void mmb_sincos2pi(double u, double* s, double* c) {
 }
 
 /* ------------------------------------------------------------------ normals */
-MMB_HD void mmb_normal_pair(const mmb_rng* s, uint32_t q, double* z0, double* z1) {
-  uint64_t a, b;
-  mmb_rng_block(s, q, &a, &b);
+/* Box-Muller of one Philox block (a, b): the pair mmb_normal_pair returns */
+MMB_HD void mmb_normal_pair_bits(uint64_t a, uint64_t b, double* z0, double* z1) {
   double u0 = mmb_u01(a), u1 = mmb_u01(b);
   double r = sqrt(-2.0 * mmb_log(1.0 - u0));
   double sn, cs;
   mmb_sincos2pi(u1, &sn, &cs);
   *z0 = r * cs;
   *z1 = r * sn;
+}
+MMB_HD void mmb_normal_pair(const mmb_rng* s, uint32_t q, double* z0, double* z1) {
+  uint64_t a, b;
+  mmb_rng_block(s, q, &a, &b);
+  mmb_normal_pair_bits(a, b, z0, z1);
 }
 MMB_HD double mmb_normal(const mmb_rng* s, uint32_t k) {
   double z0, z1;

@@ -21,15 +21,18 @@
 // Draw order (Appendix A.2): d normals for r, 1 uniform for logu0, per doubling 1 uniform
 // for the direction, 1 uniform per merge (only when the first half's s is true), 1 top-level
 // uniform only if T.s (the `&&` short-circuit of nuts.jl:117).  nutsepsilon (nuts.jl:192-205)
-// consumes d normals of the INIT substream at the first update.  Depth is capped at
-// MMB_NUTS_MAX_DEPTH = 16 (65536 leapfrogs; reference: unbounded), identically in
-// oracle/oracle.c; every update that reaches the cap with the trajectory still growing is
-// counted (Env::stat[1], mmb_nuts_stats), so a run shows whether the cap ever acted.
+// consumes d normals of the INIT substream at the first update.  The reference's doubling
+// loop is unbounded (nuts.jl:106-125); here depth stops at MMB_NUTS_MAX_DEPTH = 30, the
+// largest tree the int32 leaf index / level mask address (2^30 leapfrogs in one update, ~10^9
+// gradients: no run that finishes reaches it), identically in oracle/oracle.c.  The frames
+// are in HBM (31 slots x 3 vectors per chain), so the depth costs memory, not registers.
+// Every update that reaches the cap with the trajectory still growing is counted
+// (Env::stat[1], mmb_nuts_stats), so a run shows whether the cap ever acted.
 #pragma once
 #include "device.h"
 
 #ifndef MMB_NUTS_MAX_DEPTH
-#define MMB_NUTS_MAX_DEPTH 16
+#define MMB_NUTS_MAX_DEPTH 30
 #endif
 #define MMB_NUTS_NSLOT (MMB_NUTS_MAX_DEPTH + 1)
 

@@ -563,6 +563,9 @@ struct Smp {
       constexpr bool CHECKED = decltype(checked_c)::value;
 #endif
       uint64_t needm = 0;  // wave-uniform: nonzero if a step of this pass was not decided exactly
+      bool needl = false;  // per-lane form of needm (a lane mask: the OR stays on the scalar unit)
+      double inf_s = __builtin_inf();
+      asm volatile("" : "+s"(inf_s));  // +inf in an SGPR pair: one v_mov_b64 per pivot
 #pragma unroll
       for (int j = 0; j < DMAX; ++j) {
         if (live && j < d) {
@@ -581,7 +584,9 @@ struct Smp {
           const uint64_t eq = __ballot(key == mx);
           uint32_t elo = (uint32_t)eq, ehi = (uint32_t)(eq >> 32);
           int p = 0;
-          bool pos = mx >= 0;  // dpstf2's ajj <= 0 stop: every candidate negative
+          // one compare for the stop and the bookkeeping's ballot (pos = the complement mask)
+          const uint64_t negm = __ballot(mx < 0);
+          bool pos = __builtin_amdgcn_inverse_ballot_w64(~negm);  // dpstf2's ajj <= 0 stop
           bool fast = true;
 #ifdef MMB_PCHOL_ONECOPY
           {
@@ -629,7 +634,10 @@ struct Smp {
           if (!NOBR && !pos) {
             live = false;  // rank = pivots taken, counted after the loop
           } else {
-            const bool piv = lane == p;
+            // optimistic pass: the pivot is the lane holding the maximal high word (unique, or
+            // the pass is redone; a stopping chain's garbage step may take several of its done /
+            // out-of-range -inf lanes, which changes nothing that is used)
+            const bool piv = CHECKED ? lane == p : key == mx;
             if (piv) {
               pks[j] = p;
               if (j + 1 < d) {  // the last step has no rows left to update: no readers
@@ -653,7 +661,7 @@ struct Smp {
               prow[RI] = rinv;
               Lrow[j] = ajj;
               pe = j;
-              work = __builtin_inf();
+              work = inf_s;
               done = true;
             }
             grp_sync();
@@ -673,6 +681,20 @@ struct Smp {
               double pB = j > 16 ? prow[16 + (lane & 15)] : 0.0;
               asm volatile("" : "+v"(sig), "+v"(rinv), "+v"(pA));
               if (j > 16) asm volatile("" : "+v"(pB));
+#ifdef MMB_EXP_MUL01
+              // the first two products by plain multiplies of a broadcast read of the row's first
+              // pair (fma(a, b, 0) and a * b are the same value): no accumulator zeroing per step
+              if (j > 0) {
+                const double2 p01 = *(const double2*)prow;
+                t0 = p01.x * Lrow[0];
+                if (j > 1) t1 = p01.y * Lrow[1];
+#pragma unroll
+                for (int k = 2; k < j; ++k) {
+                  const double src = k < 16 ? pA : pB;
+                  if (k & 1) fmac_rowbc_nf(t1, src, Lrow[k], k & 15, k == 2 || k == 16);
+                  else fmac_rowbc_nf(t0, src, Lrow[k], k & 15, k == 2 || k == 16);
+                }
+#else
               if (j > 0) {
 #pragma unroll
                 for (int k = 0; k < j; ++k) {
@@ -680,6 +702,7 @@ struct Smp {
                   if (k & 1) fmac_rowbc_n(t1, src, Lrow[k], k & 15);
                   else fmac_rowbc_n(t0, src, Lrow[k], k & 15);
                 }
+#endif
               }
               const double lij = (sig - (t0 + t1)) * rinv;
               // done lanes carry work = +inf, which absorbs lij^2: no select for work
@@ -700,15 +723,19 @@ struct Smp {
 #endif
             const uint64_t bad = __ballot(!(dl < BIG));                     // NaN, +inf, >= 2^700
             const uint64_t tiny = __ballot((uint32_t)mx < (uint32_t)KEY_LO);  // 0 <= max < 2^-700
-            const uint64_t neg = __ballot(mx < 0);
+            const uint64_t neg = negm;
             uint32_t nlo = (uint32_t)neg, nhi = (uint32_t)(neg >> 32);
             asm("" : "+s"(elo), "+s"(ehi), "+s"(nlo), "+s"(nhi));
-            // (a stopping chain's -inf keys tie: ignored)
+            // (a stopping chain's -inf keys tie: ignored.  A live lane cannot share the done lanes'
+            // -inf key here: with every diagonal below 2^700 and every pivot above 2^-700, as this
+            // pass checks, |lij| <= sqrt(Sigma_ll) < 2^350 for the PSD moment matrix, so work
+            // stays finite; a -inf diagonal needs an overflowed Mv^2, whose Mvv is inf too: NaN.)
             const uint32_t tie = ((elo & (elo - 1)) & (nlo ? 0u : ~0u)) | ((ehi & (ehi - 1)) & (nhi ? 0u : ~0u));
-            needm |= bad | tiny | (uint64_t)tie;
+            needl = needl | __builtin_amdgcn_inverse_ballot_w64(bad | tiny | (tie ? ~0ull : 0ull));
           }
         }
       }
+      needm |= __ballot(needl);
       return needm != 0;
     };
 #if defined(MMB_PCHOL_ONECOPY)

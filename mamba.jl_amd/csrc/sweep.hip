@@ -9,6 +9,7 @@
 // pivoted Cholesky factor are staged in LDS.
 #include "samplers.h"
 #include "ir.h"
+#include <cstdlib>
 
 #ifdef MMB_PHASE_PROF
 #include <cstdio>
@@ -149,6 +150,8 @@ static hipError_t launch(const SweepArgs& A, hipStream_t st, int threads) {
   return hipGetLastError();
 }
 
+hipError_t mmb_launch_line_amm(const SweepArgs& A, hipStream_t st);  // line_amm.hip
+
 // host-side launcher (engine.cpp); kinds = bitmask of the scheme's sampler kinds
 #ifndef MMB_RATS_BLOCK
 #define MMB_RATS_BLOCK 256
@@ -162,6 +165,10 @@ hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipSt
   }
   if (model == MMB_MODEL_IR) return launch<MMB_MODEL_IR, K_IR>(A, st, 128);
   if (model == MMB_MODEL_LINE) {
+    // one AMM block (BASELINE configs[1]): four lanes per chain, tune state in registers
+    // (line_amm.hip); bit-identical to the generic kernel, which MMB_LINE_GENERIC=1 selects
+    if (kinds == (1u << MMB_SAMPLER_AMM) && A.nb == 1 && !std::getenv("MMB_LINE_GENERIC"))
+      return mmb_launch_line_amm(A, st);
     if (kinds & K_GRAD) return launch<MMB_MODEL_LINE, K_ALL_GRAD>(A, st, 64);
     return launch<MMB_MODEL_LINE, K_ALL>(A, st, 64);
   }
