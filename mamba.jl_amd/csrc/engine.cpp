@@ -568,6 +568,7 @@ static void free_dev(mmb_engine* e) {
 
 #ifdef MMB_PHASE_PROF
 void mmb_prof_dump();
+void mmb_prof_dump_line();
 #endif
 
 void mmb_destroy(mmb_engine* e) {
@@ -576,6 +577,7 @@ void mmb_destroy(mmb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
 #ifdef MMB_PHASE_PROF
   mmb_prof_dump();
+  mmb_prof_dump_line();
 #endif
 #ifdef MMB_PCHOL_COUNT
   if (e->d_nstat) {
