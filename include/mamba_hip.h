@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 5
+#define MMB_ABI_VERSION 6
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -79,6 +79,15 @@ typedef enum { MMB_ADAPT_ALL = 0, MMB_ADAPT_BURNIN = 1, MMB_ADAPT_NONE = 2 } mmb
 typedef enum { MMB_SLICE_MULTIVARIATE = 0, MMB_SLICE_UNIVARIATE = 1 } mmb_slice_form;
 
 /* One sampling block = one Sampler in Model.samplers (src/Mamba.jl:119-124). */
+/* Gradient of a NUTS / HMC / MALA block.  The reference differentiates logpdf! with Calculus
+ * (gradlogpdf!(m, x, block, transform; dtype = :forward), simulation.jl:47-51): forward
+ * differences with epsilon = sqrt(eps()) * max(1, |x_i|), non-finite entries -> 0.
+ *   MMB_GRAD_DEFAULT  the model's default: forward differences on line and the node IR (the
+ *                     reference's), the analytic gradient kernel on logistic (configs[3])
+ *   MMB_GRAD_FORWARD  forward differences (line, node IR; logistic: MMB_E_ARG)
+ *   MMB_GRAD_ANALYTIC the hand-derived gradient (line, logistic; node IR: MMB_E_ARG) */
+typedef enum { MMB_GRAD_DEFAULT = 0, MMB_GRAD_FORWARD = 1, MMB_GRAD_ANALYTIC = 2 } mmb_gradient;
+
 typedef struct {
   int32_t sampler;                         /* mmb_sampler_kind */
   int32_t nnodes;                          /* number of nodes in `params` */
@@ -96,7 +105,7 @@ typedef struct {
                                               | HMC/MALA Sigma[dim*dim] col-major, or none (SigmaL = I) */
   double epsilon;                          /* HMC/MALA step size (hmc.jl:13, mala.jl:12) */
   int32_t nsteps;                          /* HMC leapfrog steps L (hmc.jl:13) */
-  int32_t reserved;
+  int32_t gradient;                        /* NUTS/HMC/MALA logpdfgrad! (sampler.jl:97-111): mmb_gradient */
 } mmb_block_spec;
 
 typedef struct {

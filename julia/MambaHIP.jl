@@ -26,6 +26,7 @@ const MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = Int32(1), Int32(2), I
 const MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE = Int32(1), Int32(2), Int32(3), Int32(4)
 const MMB_SAMPLER_GIBBS, MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = Int32(5), Int32(6), Int32(7)
 const MMB_ADAPT = Dict(:all => Int32(0), :burnin => Int32(1), :none => Int32(2))
+const MMB_GRAD_DEFAULT = Int32(0)   # mmb_gradient: the model's default (:forward on line / node IR)
 const MMB_COMM_ID_BYTES = 128
 
 # ---- structs (layout-checked against the header by tests/test_abi.py on the Python side) ----
@@ -34,7 +35,7 @@ immutable BlockSpec                      # mmb_block_spec
   adapt::Int32; form::Int32; transform::Int32; batchsize::Int32
   target::Float64; beta::Float64; scale::Float64
   dim::Int32; ntuning::Int32; tuning::Ptr{Float64}
-  epsilon::Float64; nsteps::Int32; reserved::Int32
+  epsilon::Float64; nsteps::Int32; gradient::Int32
 end
 const NOBLOCK = BlockSpec(0, 0, (0, 0, 0, 0), 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 0, C_NULL, 0.0, 0, 0)
 
@@ -190,7 +191,7 @@ function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::In
   isa(s.tune, TUNE_OF[r.kind]) || return nothing
   blk(adapt_, form, transform, batchsize, target, beta, scale, tun, eps, L) =
     BlockSpec(r.kind, nnodes, nodes, adapt_, form, transform, batchsize, target, beta, scale, dim,
-              length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L, 0)
+              length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L, MMB_GRAD_DEFAULT)
   adapt = MMB_ADAPT[kwarg(r, :adapt, :none)]
   if r.kind == MMB_SAMPLER_GIBBS
     return blk(MMB_ADAPT[:none], 0, 0, 0, 0.0, 0.0, 0.0, Float64[], 0.0, 0)
@@ -203,6 +204,9 @@ function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::In
     size(r.pargs[1], 1) == dim || throw(ArgumentError("Sigma dimension differs from variate length $dim"))
     return blk(adapt, 0, 1, 0, 0.0, kwarg(r, :beta, 0.05), kwarg(r, :scale, 2.38), Sig, 0.0, 0)
   elseif r.kind == MMB_SAMPLER_NUTS                                            # nuts.jl:5-39
+    # the device differentiates with :forward differences (Calculus, simulation.jl:47-51) or, on
+    # the logistic kernel, analytically; any other dtype keeps the Julia path
+    kwarg(r, :dtype, :forward) == :forward || return nothing
     return blk(MMB_ADAPT[:burnin], 0, 1, 0, kwarg(r, :target, 0.6), 0.0, 0.0, Float64[], 0.0, 0)
   elseif r.kind == MMB_SAMPLER_SLICE                                           # slice.jl:7-26
     w = fillvec(r.pargs[1], dim); push!(keep, w)
@@ -210,6 +214,7 @@ function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::In
     form = r.pargs[2] == Univariate ? Int32(1) : Int32(0)
     return blk(MMB_ADAPT[:none], form, Int32(kwarg(r, :transform, false)), 0, 0.0, 0.0, 0.0, w, 0.0, 0)
   else                                                                         # hmc.jl:5-32, mala.jl:5-30
+    kwarg(r, :dtype, :forward) == :forward || return nothing
     hmc = r.kind == MMB_SAMPLER_HMC
     nS = hmc ? 3 : 2                                  # (epsilon, L[, Sigma]) / (epsilon[, Sigma])
     S = length(r.pargs) >= nS ? vec(Float64[r.pargs[nS]...]) : Float64[]; push!(keep, S)

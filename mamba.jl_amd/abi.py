@@ -13,7 +13,8 @@ MMB_MAX_NODES_PER_BLOCK = 4
 MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC, MMB_MODEL_IR = 1, 2, 3, 4
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
-MMB_ABI_VERSION = 5
+MMB_ABI_VERSION = 6
+MMB_GRAD_DEFAULT, MMB_GRAD_FORWARD, MMB_GRAD_ANALYTIC = 0, 1, 2
 MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
 MMB_SLICE_MULTIVARIATE, MMB_SLICE_UNIVARIATE = 0, 1
@@ -41,7 +42,7 @@ class BlockSpec(C.Structure):
                 ("form", C.c_int32), ("transform", C.c_int32), ("batchsize", C.c_int32),
                 ("target", C.c_double), ("beta", C.c_double), ("scale", C.c_double),
                 ("dim", C.c_int32), ("ntuning", C.c_int32), ("tuning", C.POINTER(C.c_double)),
-                ("epsilon", C.c_double), ("nsteps", C.c_int32), ("reserved", C.c_int32)]
+                ("epsilon", C.c_double), ("nsteps", C.c_int32), ("gradient", C.c_int32)]
 
 
 class ModelSpec(C.Structure):

@@ -80,6 +80,7 @@ struct DBlock {
   double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
   double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)
   int32_t ir_blk;        // node IR: index into SweepArgs::ir_blocks
+  int32_t fdgrad;        // NUTS/HMC/MALA on line: 1 = Calculus forward differences (mmb_gradient)
 };
 
 struct SweepArgs {

@@ -317,6 +317,18 @@ static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int d
       return fail(nullptr, MMB_E_UNSUPPORTED, "rats: alpha/beta must form their own block");
     }
     if (s.ntuning > 0) h.tuning.assign(s.tuning, s.tuning + s.ntuning);
+    // logpdfgrad! scheme of gradient samplers (mmb_gradient): forward differences where the
+    // model supports them (line, node IR), the analytic gradient on line and logistic
+    if (s.sampler == MMB_SAMPLER_NUTS || s.sampler == MMB_SAMPLER_HMC || s.sampler == MMB_SAMPLER_MALA) {
+      const int gr = s.gradient;
+      const bool ok = gr == MMB_GRAD_DEFAULT ||
+                      (gr == MMB_GRAD_FORWARD && e->model != MMB_MODEL_LOGISTIC) ||
+                      (gr == MMB_GRAD_ANALYTIC && e->model != MMB_MODEL_IR);
+      if (!ok) {
+        delete e;
+        return fail(nullptr, MMB_E_ARG, "block %d: gradient %d is not available for this model", b, gr);
+      }
+    }
     switch (s.sampler) {
       case MMB_SAMPLER_AMWG:
         if (!(s.ntuning == 1 || s.ntuning == d)) {
@@ -742,6 +754,8 @@ static int upload_blocks(mmb_engine* e) {
     d.adapt = h.spec.adapt;
     d.batchsize = h.spec.batchsize;
     d.sigl_diag = h.sigl_diag;
+    // forward differences (the reference's default) unless the analytic gradient was asked for
+    d.fdgrad = h.spec.gradient != MMB_GRAD_ANALYTIC ? 1 : 0;
     for (int a = 0; a < 4; ++a) d.nodes[a] = a < h.spec.nnodes ? h.spec.nodes[a] : -1;
     // line: element -> value index (beta -> 0,1; s2 -> 2)
     int o = 0;

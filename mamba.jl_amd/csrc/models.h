@@ -377,9 +377,29 @@ struct Mdl<MMB_MODEL_LINE> {
     }
     return lp + ylp(A, s);  // targets: mu (logical, 0), y
   }
-  // analytic gradient (reference: Calculus forward differences, simulation.jl:47-51)
+  // logpdfgrad!(block, x, dtype) (sampler.jl:106-111): B.fdgrad -> the reference's Calculus
+  // forward differences (simulation.jl:47-51; epsilon = sqrt(eps()) * max(1, |x_i|), Julia max
+  // propagating NaN; (f(x + epsilon e_i) - f(x)) / epsilon), else the analytic gradient;
+  // non-finite entries -> 0 either way
   __device__ __forceinline__ static double logf_grad(const SweepArgs& A, const DBlock& B, const St& s0,
                                      const double* x, double* gr) {
+    if (B.fdgrad) {
+      Grp<G> g;
+      const double fx = logf(A, B, s0, Lc{}, g, x);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        double gk = 0.0;
+        if (k < B.d) {
+          const double ax = fabs(x[k]);
+          const double eps = 0x1p-26 * (isnan(ax) ? ax : (ax > 1.0 ? ax : 1.0));
+          double xx[3] = {x[0], x[1], x[2]};
+          xx[k] = x[k] + eps;
+          gk = (logf(A, B, s0, Lc{}, g, xx) - fx) / eps;
+        }
+        gr[k] = isfinite(gk) ? gk : 0.0;
+      }
+      return fx;
+    }
     St s = s0;
     Grp<G> g;
     relist(B, s, g, x);

@@ -109,7 +109,7 @@ class Model:
             bs.adapt, bs.form, bs.transform = s.adapt, s.form, s.transform
             bs.batchsize, bs.target, bs.beta, bs.scale = s.batchsize, s.target, s.beta, s.scale
             bs.dim = self.block_dim(s)
-            bs.epsilon, bs.nsteps = s.epsilon, s.nsteps
+            bs.epsilon, bs.nsteps, bs.gradient = s.epsilon, s.nsteps, s.gradient
             if s.tuning is not None:
                 t = np.ascontiguousarray(s.tuning, dtype=np.float64)
                 keep.append(t)

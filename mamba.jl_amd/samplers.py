@@ -52,6 +52,7 @@ class Sampler:
         self.scale = float(kw.pop("scale", 2.38))
         self.epsilon = float(kw.pop("epsilon", 0.0))
         self.nsteps = int(kw.pop("nsteps", 0))
+        self.gradient = int(kw.pop("gradient", abi.MMB_GRAD_DEFAULT))
         if kw:
             raise ArgumentError(f"unsupported sampler arguments {sorted(kw)}")
         self.targets = []
@@ -88,15 +89,23 @@ def AMM(params, Sigma, adapt="all", beta=0.05, scale=2.38):
 
 
 def NUTS(params, dtype="forward", target=0.6):
-    _dtype(dtype)
-    return Sampler(params, abi.MMB_SAMPLER_NUTS, abi.MMB_ADAPT_BURNIN, None, target=target)
+    return Sampler(params, abi.MMB_SAMPLER_NUTS, abi.MMB_ADAPT_BURNIN, None, target=target,
+                   gradient=_dtype(dtype))
 
 
 def _dtype(dtype):
-    # dtype selects Calculus' finite-difference scheme in the reference; the lowered
-    # models supply analytic gradients, so it is accepted and ignored.
-    if str(dtype).lstrip(":") not in ("forward", "central", "complex"):
-        raise ArgumentError(f"unsupported dtype {dtype}")
+    """logpdfgrad! scheme (sampler.jl:97-111 -> simulation.jl:47-51, Calculus): "forward" (the
+    reference's default) -> MMB_GRAD_DEFAULT: forward differences on line and the node IR, the
+    analytic gradient kernel on logistic (configs[3]); "analytic" -> the hand-derived gradient
+    (line, logistic).  Calculus' :central / :complex are not on the device."""
+    d = str(dtype).lstrip(":")
+    if d == "forward":
+        return abi.MMB_GRAD_DEFAULT
+    if d == "analytic":
+        return abi.MMB_GRAD_ANALYTIC
+    if d in ("central", "complex"):
+        raise ArgumentError(f"dtype :{d} is not supported on the device (forward or analytic)")
+    raise ArgumentError(f"unsupported dtype {dtype}")
 
 
 def _sigma(Sigma):
@@ -110,17 +119,17 @@ def _sigma(Sigma):
 
 def HMC(params, epsilon, L, Sigma=None, dtype="forward"):
     """HMC(params, epsilon, L[, Sigma]; dtype) -- hmc.jl:47-55; tune [epsilon, L] (HMCTune)."""
-    _dtype(dtype)
+    g = _dtype(dtype)
     if int(L) != L:
         raise ArgumentError("L must be an integer")
     return Sampler(params, abi.MMB_SAMPLER_HMC, abi.MMB_ADAPT_NONE, _sigma(Sigma), epsilon=epsilon,
-                   nsteps=int(L))
+                   nsteps=int(L), gradient=g)
 
 
 def MALA(params, epsilon, Sigma=None, dtype="forward"):
     """MALA(params, epsilon[, Sigma]; dtype) -- mala.jl:43-51; tune [epsilon] (MALATune)."""
-    _dtype(dtype)
-    return Sampler(params, abi.MMB_SAMPLER_MALA, abi.MMB_ADAPT_NONE, _sigma(Sigma), epsilon=epsilon)
+    g = _dtype(dtype)
+    return Sampler(params, abi.MMB_SAMPLER_MALA, abi.MMB_ADAPT_NONE, _sigma(Sigma), epsilon=epsilon, gradient=g)
 
 
 def Slice(params, width, form=Multivariate, transform=False):

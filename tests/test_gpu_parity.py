@@ -50,6 +50,11 @@ LINE_SCHEMES = {
     "mala": lambda M: [M.MALA(["beta", "s2"], 0.01)],
     "mala_sigma_gibbs": lambda M: [M.MALA("beta", 0.3, np.array([[1.6, -0.45], [-0.45, 0.15]])),
                                    M.Gibbs("s2")],
+    # the reference's default gradient is Calculus :forward differences (the schemes above);
+    # dtype="analytic" selects the hand-derived one
+    "nuts_analytic": lambda M: [M.NUTS(["beta", "s2"], dtype="analytic")],
+    "hmc_analytic": lambda M: [M.HMC(["beta", "s2"], 0.05, 8, dtype="analytic")],
+    "mala_analytic_gibbs": lambda M: [M.MALA("beta", 0.3, dtype="analytic"), M.Gibbs("s2")],
 }
 
 
@@ -587,3 +592,23 @@ def test_rats_scale_total_on_one_gpu(mamba, oracle):
     st = oracle.new_state(m, init[:32])
     do = oracle.run(m, st, 24, burnin=0, thin=4, seed=8, chain_offset=0, nthreads=8)
     np.testing.assert_allclose(d[:, :, :32], do, rtol=1e-9, atol=1e-9)
+
+
+def test_gradient_choice_validated(mamba):
+    """mmb_gradient (include/mamba_hip.h): forward differences are not available on the logistic
+    kernel, the analytic gradient not on the node IR; both are refused at mmb_create."""
+    A = mamba.abi
+    m = mamba.logistic(200, 5, 10.0)
+    s = mamba.NUTS("beta")
+    s.gradient = A.MMB_GRAD_FORWARD
+    m.setsamplers([s])
+    with pytest.raises(RuntimeError, match="gradient"):
+        mamba.Engine(m)
+    ir = mamba.ir
+    mi = ir.seeds_model().setinputs(ir.SEEDS)
+    mi.setsamplers([mamba.NUTS(["alpha0", "alpha1", "alpha2", "alpha12"], dtype="analytic"), mamba.AMWG("b", 0.01),
+                    mamba.AMWG("s2", 0.1)])
+    with pytest.raises(RuntimeError, match="gradient"):
+        mamba.Engine(mi)
+    with pytest.raises(mamba.samplers.ArgumentError):
+        mamba.NUTS("beta", dtype="central")

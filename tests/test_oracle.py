@@ -67,7 +67,7 @@ def test_logistic_logpdf_and_gradient_golden(mamba, oracle):
 
 
 def test_line_gradient_golden(mamba, oracle):
-    m = line_model(mamba, [mamba.NUTS("beta"), mamba.NUTS(["beta", "s2"])])
+    m = line_model(mamba, [mamba.NUTS("beta", dtype="analytic"), mamba.NUTS(["beta", "s2"], dtype="analytic")])
     for c in load("logpdf.json")["line_grad"]:
         v = c["vals"]
         _, g1 = oracle.block_logpdf(m, v, 0, v[:2], grad=True)
@@ -75,6 +75,28 @@ def test_line_gradient_golden(mamba, oracle):
         _, g2 = oracle.block_logpdf(m, v, 1, [v[0], v[1], np.log(v[2])], grad=True)
         np.testing.assert_allclose(g2[:2], c["grad_beta"], rtol=1e-11)
         assert g2[2] == pytest.approx(c["grad_ls2"], rel=1e-10)
+
+
+def test_line_forward_difference_gradient(mamba, oracle):
+    """The reference's default gradient (dtype=:forward, simulation.jl:47-51 -> Calculus
+    finite_difference!): g_i = (f(x + e_i eps_i) - f(x)) / eps_i, eps_i = sqrt(eps()) * max(1, |x_i|),
+    restated here from the oracle's own block logpdf (bit-exact), and within forward-difference
+    accuracy of the analytic golden gradient (pinned by scipy in tests/golden/logpdf.json)."""
+    m = line_model(mamba, [mamba.NUTS("beta"), mamba.NUTS(["beta", "s2"])])
+    for c in load("logpdf.json")["line_grad"]:
+        v = c["vals"]
+        for blk, x in ((0, list(v[:2])), (1, [v[0], v[1], np.log(v[2])])):
+            lp, g = oracle.block_logpdf(m, v, blk, x, grad=True)
+            f0 = oracle.block_logpdf(m, v, blk, x)
+            assert lp == f0
+            for i in range(len(x)):
+                eps = 2.0 ** -26 * max(1.0, abs(x[i]))
+                xe = list(x)
+                xe[i] = x[i] + eps
+                assert g[i] == (oracle.block_logpdf(m, v, blk, xe) - f0) / eps
+            np.testing.assert_allclose(g[:2], c["grad_beta"], rtol=1e-5, atol=1e-5)
+            if blk == 1:
+                assert g[2] == pytest.approx(c["grad_ls2"], rel=1e-5, abs=1e-5)
 
 
 def test_pivoted_cholesky(oracle):
