@@ -608,6 +608,7 @@ def test_gradient_choice_validated(mamba):
     mi = ir.seeds_model().setinputs(ir.SEEDS)
     mi.setsamplers([mamba.NUTS(["alpha0", "alpha1", "alpha2", "alpha12"], dtype="analytic"), mamba.AMWG("b", 0.01),
                     mamba.AMWG("s2", 0.1)])
+    mi.init_matrix([ir.seeds_inits()[0]], 1)
     with pytest.raises(RuntimeError, match="gradient"):
         mamba.Engine(mi)
     with pytest.raises(mamba.samplers.ArgumentError):
