@@ -368,7 +368,7 @@ def main():
                 "window": f"timed run: {args.steps} iterations, burnin {tburn}"}
     else:
         W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
-                               "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "64"))
+                               "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "256"))
         nroof = max(W * 16, 64)
         eng.run(nroof, burnin=0, thin=thin, model_burnin=0, draws=False, keep_device=False, time_kernels=True)
         kms, launches, units = eng.kernel_time()
