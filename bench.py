@@ -383,6 +383,10 @@ def main():
                 "avg_launch_ms": avg_ms, "launches": launches, "chain_updates_per_launch": units / launches}
         if tsrc:
             roof["traffic_source"] = tsrc
+        if args.workload == "line_amm" and not os.environ.get("MMB_LINE_GENERIC"):
+            # one AMM block: the engine runs the four-lanes-per-chain kernel (csrc/line_amm.hip);
+            # latency-bound (256 waves on 1,024 SIMDs), so the HBM fraction is a floor, not a target
+            roof["kernel"] = "line_amm_kernel"
         if args.workload == "rats" and args.scheme == "reference" and os.path.exists(VALU_FILE):
             # f1 row: bound by FP64 vector issue, not HBM (SURVEY §8(d) row 3'); HBM kept alongside
             v = json.load(open(VALU_FILE))

@@ -23,7 +23,7 @@
 // The moments, Sigma, the factorization's pivot replay and dot products keep the generic
 // kernel's operation order, so the draws, the tune state and the factor are bit-identical to
 // sweep_kernel<LINE> and to oracle/oracle.c (tests/test_gpu_line_amm.py at the configuration's
-// 4,096 chains).  Measured: 5.39e8 chain-updates/s vs 2.57e8 for the generic kernel (2.1x).
+// 4,096 chains).  Measured: 5.61e8 chain-updates/s vs 2.57e8 for the generic kernel (2.2x).
 // The engine uses this kernel for a line scheme that is one AMM block (any d <= 3, emap,
 // transform, sigl, adapt); MMB_LINE_GENERIC=1 selects the generic kernel.
 #include "samplers.h"
