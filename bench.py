@@ -320,6 +320,7 @@ def main():
     # a Julia caller uses); rank 0's unique id travels over the launcher's process group.
     # MMB_DIST_BACKEND=gloo (several ranks sharing one GPU, which RCCL refuses) reduces the same
     # device partials through torch.distributed on the host instead.
+    psrf, coll_note = None, None
     if backend == "nccl":
         # RCCL prints a version banner on stdout at communicator init: keep stdout for the one
         # JSON line (the banner goes to stderr)
@@ -333,11 +334,17 @@ def main():
             comm = mb.Comm([eng], nranks=world, rank0=rank, uid=uid[0])
             psrf, _ = mb.gelmandiag_rccl(comm)
             comm.close()
+        except Exception as ex:  # noqa: BLE001 -- the timed throughput above stands either way
+            # a failing library communicator (init is collective: every rank sees it) falls back
+            # to the same device partials reduced through torch.distributed, and says so
+            coll_note = f"library RCCL communicator failed ({type(ex).__name__}: {ex}); partials " \
+                        "reduced through torch.distributed instead"
+            print(f"bench: {coll_note}", file=sys.stderr)
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
-    else:
+    if psrf is None:
         def ar_sum(x):
             t = torch.tensor(x, dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t)
@@ -420,7 +427,9 @@ def main():
                  else
                  "synthetic X ~ N(0,1), y ~ Bernoulli(invlogit(X beta_true)) (SURVEY §8d seeds); inits N(0, 0.1^2)"),
         "config": {"workload": desc, "chains_per_gpu": K, "global_chains": K * world, "thin": thin,
-                   "parallelism": f"chain-shard x{world}", "collective": ("rccl (mmb_gr_allreduce)" if backend == "nccl" else backend)},
+                   "parallelism": f"chain-shard x{world}",
+                   "collective": ("rccl (mmb_gr_allreduce)" if backend == "nccl" and coll_note is None else
+                                  f"{backend} (torch.distributed)")},
         "roofline": roof,
     }
     if args.workload != "rats":
@@ -434,6 +443,8 @@ def main():
         out["nuts"] = nuts_timed
     if psrf is not None:
         out["gelman_rubin_psrf"] = [float(x) for x in psrf[:, 0]]
+    if coll_note is not None:
+        out["config"]["collective_note"] = coll_note
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if args.workload == "rats":
             ref = rats_model(mb, scheme_for(mb, "reference"))
