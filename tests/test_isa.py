@@ -86,7 +86,9 @@ def test_dpp_sources_have_wait_states(tmp_path):
 
 
 def test_isa_census_finds_the_factorization_steps():
-    """tools/isa_census.py locates the 30 steps of the rats factorization (step j: j DPP fmacs)."""
+    """tools/isa_census.py locates the steps of the rats factorization (step j: j DPP fmacs).  The
+    rats kernel's copy with d = 30 a compile-time constant has no dot product at its last step
+    (no rows left), so the run it finds ends at step 28 (29 steps); a runtime-d copy shows 30."""
     if not os.path.exists(OBJ) or not os.path.exists(os.path.join(LLVM, "llvm-objdump")):
         pytest.skip("no in-tree build object or ROCm LLVM tools")
     import importlib.util
@@ -95,6 +97,6 @@ def test_isa_census_finds_the_factorization_steps():
     spec.loader.exec_module(ic)
     ins = ic.kernel_instructions(ic.disassemble())
     steps = ic.factorization_steps(ins)
-    assert len(steps) == 30
+    assert len(steps) in (29, 30)
     for j, (lo, hi) in enumerate(steps):
         assert sum(1 for mn, _ in ins[lo:hi] if mn == "v_fmac_f64_dpp") == j
