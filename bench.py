@@ -11,8 +11,16 @@ mmb_run window (kernels of 8 iterations); state and data are resident in HBM.
 
 Steady state: before --warmup, an untimed adaptation pre-run (--adapt-prerun, default
 128 >= 2d+2 = 62 for the 30-d AMM blocks) takes every chain past AMM's switch to the
-adaptive proposal (tune.m > 2n, amm.jl:73-75), so the timed steps run the configuration
-they name: mixture proposal + full-rank pivoted Cholesky (amm.jl:72-90) every update.
+mixture proposal (tune.m > 2n, amm.jl:73-75), so every timed update runs the mixture
+proposal and a pivoted Cholesky of the moment matrix (amm.jl:72-90).  That factorization does
+NOT reach full rank in every chain: setadapt!'s `tune.Mv = v` alias (amm.jl:102) makes the
+first adaptive update's Mvv - Mv Mv' = (v0 v0' - v1 v1') / 2, indefinite whenever that first
+proposal was accepted (about half the alpha chains, a third of the beta chains), and the running
+averages shrink it only like 2/(m+1); dpstf2 stops after a few pivots in those chains every
+update and their SigmaLm stays zero (amm.jl:88-90, 104; pinned by tests/test_oracle.py::
+test_rats_amm_alias_leaves_first_accepted_chains_without_factor).  The line therefore reports,
+per AMM block over the timed window, the full-rank fraction, the mean rank and the mean
+factorization steps the device executed (config.amm, from mmb_amm_stats).
 The timed window's own kernel time (HIP events on the engine stream) is checked against
 its wall time: the run fails if kernel ms per step exceeds ms_per_step by > 5 %.
 
@@ -215,6 +223,28 @@ def setup_workload(mb, args, rank):
     return model, init, "logistic N=10000 p=50 NUTS (BASELINE configs[3])", {"thin": 1}, "f64"
 
 
+def amm_window(model, before, after):
+    """Per AMM block, the timed window's factorization statistics (mmb_amm_stats differences):
+    the fraction of updates whose pivoted Cholesky reached rank n (SigmaLm replaced, amm.jl:88-90),
+    the mean rank, the mean factorization steps the device executed per update (the two chains
+    of a wavefront step together, so a chain that stops early still costs its partner's steps)
+    and the fraction of optimistic passes redone by the checked pass."""
+    out = {}
+    for b, a in after.items():
+        o = before.get(b, {})
+        dv = {k: a[k] - o.get(k, 0) for k in a}
+        n = dv["updates"]
+        if n <= 0:
+            continue
+        s = model.samplers[b]
+        name = ",".join(s.params) if isinstance(s.params, (list, tuple)) else str(s.params)
+        d = model.block_dim(s)
+        out[name] = {"updates": n, "d": d, "full_rank_frac": dv["full_rank"] / n, "rank_mean": dv["rank_sum"] / n,
+                     "pchol_steps_mean": dv["steps_sum"] / n, "pchol_steps_frac": dv["steps_sum"] / (n * d),
+                     "redo_frac": dv["redo"] / n}
+    return out
+
+
 def pmc_traffic(args, W):
     """HBM bytes per sweep launch from the committed rocprofv3 PMC pass of this exact kernel
     build and configuration (profiles/, gathered by tools/profiles_run.sh and corrected by
@@ -291,6 +321,7 @@ def main():
         mburn = tburn = args.nuts_burnin if args.nuts_burnin is not None else args.steps // 2
     eng.reserve_draws(args.steps // thin + 1)
     nuts_before = eng.nuts_stats() if nuts else None
+    amm_before = eng.amm_stats()
     barrier()
     t0 = time.perf_counter()
     eng.run(args.steps, burnin=tburn, thin=thin, model_burnin=mburn, draws=False, keep_device=True,
@@ -310,6 +341,7 @@ def main():
         raise SystemExit(f"bench: kernel time per step {kernel_ms_per_step:.4f} ms exceeds the timed "
                          f"window's {ms_per_step:.4f} ms by more than 5 % — timing is inconsistent")
     grads_timed = eng.grad_evals() if nuts else 0  # (the counter restarts with every mmb_run)
+    amm_timed = amm_window(model, amm_before, eng.amm_stats())
     nuts_timed = None
     if nuts:
         after = eng.nuts_stats()
@@ -344,6 +376,15 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
+    if backend == "nccl" and world > 1:
+        # the fallback decision is collective too: one rank's local failure after the library's
+        # agreement step sends every rank to the torch.distributed reduction (no rank left waiting)
+        flag = torch.tensor([1.0 if psrf is None else 0.0], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if float(flag.item()) != 0.0 and psrf is not None:
+            psrf = None
+            coll_note = "library RCCL communicator failed on another rank; partials reduced through " \
+                        "torch.distributed instead"
     if psrf is None:
         def ar_sum(x):
             t = torch.tensor(x, dtype=torch.float64, device=coll_dev)
@@ -439,6 +480,8 @@ def main():
                               "scheme": args.scheme})
         if args.scheme == "gibbs_amm":
             out["config"]["amm_adapt"] = "all"
+    if amm_timed:
+        out["config"]["amm"] = amm_timed
     if nuts_timed is not None:
         out["nuts"] = nuts_timed
     if psrf is not None:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 6
+#define MMB_ABI_VERSION 7
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -322,6 +322,19 @@ int mmb_grad_evals(mmb_engine* e, int64_t* n);
  * reference's unbounded doubling loop (nuts.jl:106-125) would have continued, out[2] = sum of
  * final tree depths j.  out[1] == 0 means the cap never changed a draw. */
 int mmb_nuts_stats(mmb_engine* e, int64_t out[3]);
+/* AMM factorization statistics since mmb_init_chains, per sampling block b (zero rows for
+ * non-AMM blocks), summed over the engine's chains: out[b*MMB_AMM_STATS + i] =
+ *   i = 0  adaptive updates, i.e. cholfact(Hermitian(Sigma), Val{true}) calls (amm.jl:81-87)
+ *   i = 1  of them with rank(F) == n, i.e. SigmaLm replaced (amm.jl:88-90)
+ *   i = 2  sum of rank(F) (dpstf2's pivots taken before its ajj <= 0 stop)
+ *   i = 3  sum of factorization steps the device executed for the update's chain group:
+ *          min(rank + 1, n) per chain, the max over the two chains of a wavefront on the
+ *          32-lane kernels (both chains step together), the chain's own count elsewhere
+ *   i = 4  updates whose optimistic factorization pass was redone by the checked pass
+ * Diagnostics only (the bench reports the full-rank fraction and mean steps of its timed
+ * window); no draw depends on them. */
+#define MMB_AMM_STATS 5
+int mmb_amm_stats(mmb_engine* e, int64_t* out /* MMB_MAX_BLOCKS x MMB_AMM_STATS */);
 
 #ifdef __cplusplus
 }

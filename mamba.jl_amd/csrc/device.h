@@ -55,6 +55,9 @@ __device__ __forceinline__ void mmb_sqrt_rcp_inrange(double x, double* s, double
   *rcp = mmb_rcp_inrange(*s);
 }
 
+// AMM factorization counters per chain (mmb_amm_stats fields, padded to 32 bytes)
+#define MMB_AMM_STAT_STRIDE 8
+
 // Per-block descriptor passed in kernel arguments (constant memory, uniform access).
 struct DBlock {
   int32_t kind, nn, d, transform, form, adapt, batchsize, sigl_diag;
@@ -76,6 +79,7 @@ struct DBlock {
   double* t_xnext;       // AMM   [K][DP] next iteration's proposal minus v (samplers.h amm: formed
                          //       with the factor still in registers), valid when t_xtag[c] matches
   int64_t* t_xtag;       // AMM   [K] (xepoch << 32) | iteration the carried proposal is for
+  uint32_t* t_astat;     // AMM   [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats), diagnostics
   double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
   double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
   double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)

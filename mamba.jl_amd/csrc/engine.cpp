@@ -52,6 +52,7 @@ struct BlockHost {
   uint8_t* piv = nullptr;
   double* xnext = nullptr;   // AMM carried next proposal [K][DP] (samplers.h amm)
   int64_t* xtag = nullptr;   // AMM [K] tag of the carried proposal
+  uint32_t* astat = nullptr; // AMM [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats)
 };
 
 struct mmb_engine {
@@ -547,7 +548,7 @@ int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device
 static void free_dev(mmb_engine* e) {
   for (auto& h : e->blocks) {
     void* ptrs[] = {h.sigma, h.accept, h.Mv, h.Mvv, h.Ls, h.nuts, h.nfr, h.width, h.sigl_d, h.hmc, h.m, h.flags,
-                    h.piv, h.xnext, h.xtag};
+                    h.piv, h.xnext, h.xtag, h.astat};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
     h.sigma = h.accept = h.Mv = h.Mvv = h.Ls = h.nuts = h.nfr = h.width = h.sigl_d = h.hmc = nullptr;
@@ -555,6 +556,7 @@ static void free_dev(mmb_engine* e) {
     h.piv = nullptr;
     h.xnext = nullptr;
     h.xtag = nullptr;
+    h.astat = nullptr;
   }
   if (e->d_vals) (void)hipFree(e->d_vals);
   if (e->d_blocks) (void)hipFree(e->d_blocks);
@@ -776,6 +778,7 @@ static int upload_blocks(mmb_engine* e) {
     d.sigl = h.sigl_d;
     d.t_sigma = h.sigma; d.t_accept = h.accept; d.t_m = h.m; d.t_flags = h.flags;
     d.t_Mv = h.Mv; d.t_Mvv = h.Mvv; d.t_Ls = h.Ls; d.t_piv = h.piv; d.t_xnext = h.xnext; d.t_xtag = h.xtag; d.t_nuts = h.nuts; d.t_nfr = h.nfr;
+    d.t_astat = h.astat;
     d.t_hmc = h.hmc;
     d.ir_blk = (int32_t)b;
   }
@@ -836,6 +839,8 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
       HIPCHK(e, dalloc(&h.xnext, K * DP));
       HIPCHK(e, dalloc(&h.xtag, K));
       HIPCHK(e, hipMemset(h.xtag, 0xff, K * sizeof(int64_t)));  // -1: no carried proposal
+      HIPCHK(e, dalloc(&h.astat, K * MMB_AMM_STAT_STRIDE));
+      HIPCHK(e, hipMemset(h.astat, 0, K * MMB_AMM_STAT_STRIDE * sizeof(uint32_t)));
       HIPCHK(e, dalloc(&h.sigl_d, (size_t)h.d * h.d));
       HIPCHK(e, hipMemcpy(h.sigl_d, h.sigl.data(), h.sigl.size() * sizeof(double), hipMemcpyHostToDevice));
     } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
@@ -1511,6 +1516,23 @@ int mmb_nuts_stats(mmb_engine* e, int64_t* out) {
   return 0;
 }
 
+int mmb_amm_stats(mmb_engine* e, int64_t* out) {
+  if (!e || !out) return fail(e, MMB_E_ARG, "null argument");
+  for (int i = 0; i < MMB_MAX_BLOCKS * MMB_AMM_STATS; ++i) out[i] = 0;
+  if (e->K == 0) return 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::vector<uint32_t> h;
+  for (size_t b = 0; b < e->blocks.size(); ++b) {
+    if (!e->blocks[b].astat) continue;
+    int rc = d2h(e, h, e->blocks[b].astat, (size_t)e->K * MMB_AMM_STAT_STRIDE);
+    if (rc) return rc;
+    for (int64_t k = 0; k < e->K; ++k)
+      for (int i = 0; i < MMB_AMM_STATS; ++i) out[b * MMB_AMM_STATS + i] += h[k * MMB_AMM_STAT_STRIDE + i];
+  }
+  return 0;
+}
+
 int mmb_grad_evals(mmb_engine* e, int64_t* n) {
   if (!e || !n) return fail(e, MMB_E_ARG, "null argument");
   *n = 0;
@@ -1534,6 +1556,7 @@ struct mmb_comm {
   std::vector<double*> buf;  // per local engine: [L stats | 2p range | p shift | p link (int32) | 4 agree]
   int p = 0;
   int64_t L = 0;
+  double agree[4] = {0.0, 0.0, 0.0, 0.0};  // comm_agree's contribution (outlives its async H2D copies)
 };
 
 #define NCCLCHK(e, x)                                                                 \
@@ -1643,22 +1666,33 @@ static ncclResult_t grouped_allreduce(mmb_comm* c, size_t off, size_t n, ncclRed
 // collective, and every rank sees the same verdict: all fail together (MMB_E_STATE for too few
 // draws, MMB_E_ARG when the ranks kept different numbers of draws, which would otherwise give
 // a silently wrong PSRF) or all proceed with the common n_kept.
+// A local HIP failure while staging the contribution does not skip the collective (the peers
+// are already waiting in it): the process always joins the all-reduce and the sync, and reports
+// its error afterwards (as mmb_gr_allreduce does for launch failures).
 static int comm_agree(mmb_comm* c, int64_t need, int64_t* nkept) {
   mmb_engine* e0 = c->eng[0];
   const size_t off = (size_t)c->L + 4 * (size_t)c->p;
   int64_t lo = INT64_MAX, hi = -1;
   for (mmb_engine* e : c->eng) { lo = std::min(lo, e->n_kept); hi = std::max(hi, e->n_kept); }
-  const double mine[4] = {lo < need ? 1.0 : 0.0, -(double)lo, (double)hi, 0.0};
+  c->agree[0] = lo < need ? 1.0 : 0.0;
+  c->agree[1] = -(double)lo;
+  c->agree[2] = (double)hi;
+  c->agree[3] = 0.0;
+  int lrc = 0;
   for (size_t i = 0; i < c->eng.size(); ++i) {
-    HIPCHK(e0, hipSetDevice(c->eng[i]->device));
-    HIPCHK(e0, hipMemcpyAsync(c->buf[i] + off, mine, sizeof(mine), hipMemcpyHostToDevice, c->eng[i]->stream));
+    hipError_t st = hipSetDevice(c->eng[i]->device);
+    if (st == hipSuccess)
+      st = hipMemcpyAsync(c->buf[i] + off, c->agree, sizeof(c->agree), hipMemcpyHostToDevice, c->eng[i]->stream);
+    if (st != hipSuccess && !lrc) lrc = fail(e0, MMB_E_HIP, "agreement staging: %s", hipGetErrorString(st));
   }
   const ncclResult_t r = grouped_allreduce(c, off, 4, ncclMax);
+  double all[4] = {1.0, 0.0, 0.0, 0.0};
+  hipError_t st = hipSetDevice(e0->device);
+  if (st == hipSuccess) st = hipMemcpyAsync(all, c->buf[0] + off, sizeof(all), hipMemcpyDeviceToHost, e0->stream);
+  const int rc = comm_sync(c);
   if (r != ncclSuccess) return fail(e0, MMB_E_COMM, "agreement all-reduce: %s", ncclGetErrorString(r));
-  double all[4];
-  HIPCHK(e0, hipSetDevice(e0->device));
-  HIPCHK(e0, hipMemcpyAsync(all, c->buf[0] + off, sizeof(all), hipMemcpyDeviceToHost, e0->stream));
-  int rc = comm_sync(c);  // also keeps `mine` alive until the H2D copies are done
+  if (lrc) return lrc;
+  if (st != hipSuccess) return fail(e0, MMB_E_HIP, "agreement readback: %s", hipGetErrorString(st));
   if (rc) return rc;
   if (all[0] != 0.0)
     return fail(e0, MMB_E_STATE, "need >= %lld device-kept draws per chain on every rank (this process: %lld)",

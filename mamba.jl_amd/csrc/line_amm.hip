@@ -348,6 +348,7 @@ __global__ __launch_bounds__(64) void line_amm_kernel(const SweepArgs A) {
   ML::unlist(B, s, 0, v);
   double n0, n1, uown;
   line_draw(A, chain, A.iter0 + 1, lane, n0, n1, uown);
+  uint32_t st_fac = 0, st_full = 0, st_rank = 0, st_steps = 0, st_redo = 0;  // mmb_amm_stats
 
   for (int step = 0; step < A.n_iters; ++step) {
     MMB_PROF_START
@@ -476,7 +477,12 @@ __global__ __launch_bounds__(64) void line_amm_kernel(const SweepArgs A) {
 #pragma unroll
         for (int t = 0; t < 6; ++t) Sg[t] = S0[t];
         rank = pchol3(d, Sg, pk);
+        st_redo += 1u;
       }
+      st_fac += 1u;
+      st_full += rank == d ? 1u : 0u;
+      st_rank += (uint32_t)rank;
+      st_steps += (uint32_t)(rank < d ? rank + 1 : d);
       if (rank == d) {
 #pragma unroll
         for (int t = 0; t < 6; ++t)
@@ -503,6 +509,14 @@ __global__ __launch_bounds__(64) void line_amm_kernel(const SweepArgs A) {
 #endif
   if (lane == 0) {
     ML::store(A, c, 0, s);
+    if (B.t_astat != nullptr && st_fac != 0u) {
+      uint32_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
+      a[0] += st_fac;
+      a[1] += st_full;
+      a[2] += st_rank;
+      a[3] += st_steps;
+      a[4] += st_redo;
+    }
     B.t_m[c] = m;
     B.t_flags[c] = fl;
 #pragma unroll

@@ -416,12 +416,18 @@ struct Mdl<MMB_MODEL_LINE> {
     }
     double sb = sqrt(1000.0);
     double ivb = 1.0 / (sb * sb);
-    gr[0] = sr / s2 - s.v[0] * ivb;
-    gr[1] = sxr / s2 - s.v[1] * ivb;
-    gr[2] = B.d == 3 ? -(0.001 + 2.5) + (0.5 * ssq + 0.001) / s2 : 0.0;
+    // partials by value slot (beta0, beta1, log s2), then to block elements through emap: a
+    // block may list s2 first or hold one of the nodes only ([s2, beta], [s2])
+    const double g0 = sr / s2 - s.v[0] * ivb;
+    const double g1 = sxr / s2 - s.v[1] * ivb;
+    const double g2 = -(0.001 + 2.5) + (0.5 * ssq + 0.001) / s2;
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-      if (!isfinite(gr[k])) gr[k] = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const int vi = B.emap[k];
+      double gk = vi == 0 ? g0 : vi == 1 ? g1 : g2;
+      gk = k < B.d ? gk : 0.0;
+      gr[k] = isfinite(gk) ? gk : 0.0;
+    }
     return lp;
   }
   __device__ __forceinline__ static int gibbs_draw_kind(const DBlock&, double* a) { *a = 0.0; return 0; }

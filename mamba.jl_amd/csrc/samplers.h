@@ -448,27 +448,29 @@ struct Smp {
   __device__ __forceinline__ static int pchol32(int d, double* mat, double* prow, int* pks, const Grp<G>& g,
                                                 int* pos_out, const DBlock* NB = nullptr,
                                                 const SweepArgs& A = SweepArgs{}, int c = 0, uint32_t chain = 0,
-                                                int64_t it = 0, int b = 0, int m = 0) {
+                                                int64_t it = 0, int b = 0, int m = 0, int* redo = nullptr) {
 #ifndef MMB_PCHOL_NOFULLD
     // a block as wide as the model's DMAX (rats: both 30-d blocks) runs a copy with d a
     // compile-time constant: no per-step scalar test and branch of j against d (9.58e7 ->
     // 9.90e7 rats chain-updates/s, A/B on one box, parity unchanged)
-    if (d == DMAX) return pchol32_impl<true, true>(d, mat, prow, pks, pos_out, NB, A.seed, A.xepoch, c, chain, it, b, m);
+    if (d == DMAX)
+      return pchol32_impl<true, true>(d, mat, prow, pks, pos_out, NB, A.seed, A.xepoch, c, chain, it, b, m, redo);
 #endif
-    return pchol32_impl<true>(d, mat, prow, pks, pos_out, NB, A.seed, A.xepoch, c, chain, it, b, m);
+    return pchol32_impl<true>(d, mat, prow, pks, pos_out, NB, A.seed, A.xepoch, c, chain, it, b, m, redo);
   }
 #if !defined(MMB_PCHOL_V1) && defined(MMB_PCHOL_EXACT_NOINLINE)
   // timing experiment: the checked pass (rare) out of line (measured 13 % slower: call ABI)
   __device__ __noinline__ static int pchol32_exact(int d, double* mat, double* prow, int* pks, int* pos_out,
                                                    const DBlock* NB, uint64_t seed, int64_t xepoch, int c,
                                                    uint32_t chain, int64_t it, int b, int m) {
-    return pchol32_impl<false>(d, mat, prow, pks, pos_out, NB, seed, xepoch, c, chain, it, b, m);
+    return pchol32_impl<false>(d, mat, prow, pks, pos_out, NB, seed, xepoch, c, chain, it, b, m, nullptr);
   }
 #endif
   template <bool OPT, bool FULLD = false>
   __device__ __forceinline__ static int pchol32_impl(int d_arg, double* mat, double* prow, int* pks, int* pos_out,
                                                      const DBlock* NB, uint64_t seed, int64_t xepoch, int c,
-                                                     uint32_t chain, int64_t it, int b, int m) {
+                                                     uint32_t chain, int64_t it, int b, int m,
+                                                     int* redo_out) {
     const int d = FULLD ? DMAX : d_arg;
     const Grp<G> g;
     constexpr int RI = DMAX;  // prow[RI]: the pivot's reciprocal
@@ -569,8 +571,17 @@ struct Smp {
 #else
       constexpr bool CHECKED = decltype(checked_c)::value;
 #endif
+      // POSTHOC (default): the optimistic pass keeps no per-step bookkeeping of whether its
+      // choices were dpstf2's; everything that could make them differ is visible after the loop
+      // (see the check below the step loop).  MMB_PCHOL_STEPCHECK: the round-3 per-step check.
+#ifdef MMB_PCHOL_STEPCHECK
+      constexpr bool POSTHOC = false;
+#else
+      constexpr bool POSTHOC = !CHECKED;
+#endif
       uint64_t needm = 0;  // wave-uniform: nonzero if a step of this pass was not decided exactly
       bool needl = false;  // per-lane form of needm (a lane mask: the OR stays on the scalar unit)
+      double apiv = 1.0;   // POSTHOC: this lane's candidate when it was taken as the pivot
       double inf_s = __builtin_inf();
       asm volatile("" : "+s"(inf_s));  // +inf in an SGPR pair: one v_mov_b64 per pivot
 #pragma unroll
@@ -644,9 +655,12 @@ struct Smp {
             // optimistic pass: the pivot is the lane holding the maximal high word (unique, or
             // the pass is redone; a stopping chain's garbage step may take several of its done /
             // out-of-range -inf lanes, which changes nothing that is used)
-            const bool piv = CHECKED ? lane == p : key == mx;
+            // POSTHOC: no pivot on a stopping chain's step (its done lanes keep pe and row)
+            const bool piv = CHECKED ? lane == p
+                                     : POSTHOC ? __builtin_amdgcn_inverse_ballot_w64(eq & ~negm) : key == mx;
             if (piv) {
-              pks[j] = p;
+              if constexpr (POSTHOC) apiv = dl;  // (pks: only the checked pass replays it)
+              else pks[j] = p;
               if (j + 1 < d) {  // the last step has no rows left to update: no readers
 #pragma unroll
                 for (int k = 0; k + 1 < j; k += 2) *(double2*)(prow + k) = make_double2(Lrow[k], Lrow[k + 1]);
@@ -720,7 +734,7 @@ struct Smp {
             if (NOBR) live = live && pos;
           }
 #ifndef MMB_PCHOL_ONECOPY
-          if constexpr (!CHECKED)
+          if constexpr (!CHECKED && !POSTHOC)
 #endif
           {
             // scalar bookkeeping off the step's dependency chain (after the row update, no
@@ -742,7 +756,28 @@ struct Smp {
           }
         }
       }
-      needm |= __ballot(needl);
+      if constexpr (POSTHOC) {
+        // What the optimistic choices could get wrong, checked once after the loop:
+        // * a pivot outside the in-range square root's domain [2^-700, 2^700] -- a tiny or zero
+        //   maximum, a huge or +inf one, a positive NaN key (it would have been the maximum);
+        // * a NaN candidate that never became a pivot (dpstf2 may stop on it; its work stays NaN
+        //   to the end because NaN + x = NaN and only pivots reset work);
+        // * a high-word tie: every lane holding the maximal key became a pivot at that step, so
+        //   the chain has more done lanes than steps that took pivots (pe values 0..max_pe, each
+        //   taken once when exact: done == max_pe + 1).
+        // On a tie the rows the pass computed after it are garbage; the redo replaces them.
+        const bool inr = apiv >= 0x1p-700 && apiv <= 0x1p700;
+        uint64_t need = __ballot(inb && (done ? !inr : isnan(diag0 - work)));
+        const uint64_t dn = __ballot(done && inb);
+        const int mpe = gmax_i32((done && inb) ? pe : -1);
+        const uint64_t act = __builtin_amdgcn_read_exec();
+        const int m0 = __builtin_amdgcn_readlane(mpe, 0), m1 = __builtin_amdgcn_readlane(mpe, 32);
+        if ((uint32_t)act != 0u && __builtin_popcount((uint32_t)dn) != m0 + 1) need |= 1ull;
+        if ((act >> 32) != 0u && __builtin_popcount((uint32_t)(dn >> 32)) != m1 + 1) need |= 1ull << 32;
+        needm = need;
+      } else {
+        needm |= __ballot(needl);
+      }
       return needm != 0;
     };
 #if defined(MMB_PCHOL_ONECOPY)
@@ -776,6 +811,7 @@ struct Smp {
       // rare (a few per thousand factorizations): redo with dpstf2's exact decisions; marked
       // unlikely so the block placement moves the checked pass out of the hot code
       if (__builtin_expect(pass(std::false_type{}), 0)) {
+        if (redo_out) *redo_out = 1;
         work = inb ? 0.0 : __builtin_inf();
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) Lrow[k] = 0.0;
@@ -792,9 +828,11 @@ struct Smp {
     {
       const uint64_t dn = __ballot(done && inb);
       rank = __builtin_popcount(hi_half ? (uint32_t)(dn >> 32) : (uint32_t)dn);
+#ifdef MMB_PCHOL_STEPCHECK
       // (an optimistic stop at step 0 of a 32-element block has no done / out-of-range lane to
       // take the garbage pivot: it marked one live lane)
       if (!live && d == G && rank == 1) rank = 0;
+#endif
     }
 #else
 #pragma unroll
@@ -927,6 +965,29 @@ struct Smp {
     ii -= (mmb_tri(ii) > s) ? 1 : 0;
     i = ii;
     k = s - mmb_tri(ii);
+  }
+
+  // AMM factorization counters of one update (mmb_amm_stats): rank(F) == n (amm.jl:88), the
+  // rank, the factorization steps the group executed (min(rank + 1, n) per chain; on the 32-lane
+  // kernels the two chains of a wave step together, so the wave's count is the larger one) and
+  // whether the optimistic pass was redone.  Diagnostics: lane 0 of the group, 20 bytes.
+  __device__ __forceinline__ static void amm_count(const DBlock& B, int c, int d, int rank, int redo,
+                                                   const Grp<G>& g) {
+    const int st = rank < d ? rank + 1 : d;
+    int ws = st;
+    if constexpr (G == 32) {
+      const uint64_t act = __builtin_amdgcn_read_exec();  // the upper group may have exited (c >= K)
+      const int s0 = __builtin_amdgcn_readlane(st, 0), s1 = __builtin_amdgcn_readlane(st, 32);
+      ws = max((uint32_t)act != 0u ? s0 : 0, (act >> 32) != 0u ? s1 : 0);
+    }
+    if (g.lane == 0) {
+      uint32_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
+      a[0] += 1u;
+      a[1] += rank == d ? 1u : 0u;
+      a[2] += (uint32_t)rank;
+      a[3] += (uint32_t)ws;
+      a[4] += (uint32_t)redo;
+    }
   }
 
   // ---------------------------------------------------------------- AMM
@@ -1195,17 +1256,19 @@ struct Smp {
       int rank = d;  // timing experiment only
 #else
       int rank;
+      int redo = 0;
       const bool carry = CARRY && B.t_xtag != nullptr && B.sigl_diag;
 #ifndef MMB_PCHOL_GENERIC
       int pe = 0;
       if constexpr (G == 32 && R == 1)
-        rank = pchol32(d, mat, (double*)ia, pks, g, &pe, carry ? &B : nullptr, A, c, chain, it, b, m);
+        rank = pchol32(d, mat, (double*)ia, pks, g, &pe, carry ? &B : nullptr, A, c, chain, it, b, m, &redo);
       else
 #endif
         rank = pchol(d, mat, (double*)ia, pks, g);
 #endif
       grp_sync();
       MMB_PROF_MARK(5, g.lane)
+      if (B.t_astat != nullptr) amm_count(B, c, d, rank, redo, g);
       if (rank == d) {
         double* Ls = B.t_Ls + (size_t)c * TP;
 #pragma unroll

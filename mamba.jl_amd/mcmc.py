@@ -141,6 +141,22 @@ class Engine:
         self._chk(self.lib.mmb_nuts_stats(self.h, v))
         return {"updates": v[0], "depth_cap_hits": v[1], "depth_sum": v[2]}
 
+    def amm_stats(self):
+        """AMM factorization counters since init_chains (mmb_amm_stats), one dict per AMM block
+        (keyed by block index): adaptive updates (cholfact calls, amm.jl:87), full-rank ones
+        (rank(F) == n: SigmaLm replaced, amm.jl:88-90), the rank sum, the factorization steps
+        the device executed (per wavefront of two chains on the 32-lane kernels) and the updates
+        whose optimistic pass was redone by the checked one."""
+        v = (C.c_int64 * (abi.MMB_MAX_BLOCKS * abi.MMB_AMM_STATS))()
+        self._chk(self.lib.mmb_amm_stats(self.h, v))
+        out = {}
+        for b, blk in enumerate(self.model.samplers):
+            if getattr(blk, "kind", None) != abi.MMB_SAMPLER_AMM:
+                continue
+            r = v[b * abi.MMB_AMM_STATS:(b + 1) * abi.MMB_AMM_STATS]
+            out[b] = {"updates": r[0], "full_rank": r[1], "rank_sum": r[2], "steps_sum": r[3], "redo": r[4]}
+        return out
+
     def state_bytes(self):
         b = C.c_double()
         self.lib.mmb_state_bytes(self.h, C.byref(b))

@@ -56,6 +56,8 @@ class Oracle:
                                      C.c_double, C.c_double]
         L.orc_gamma.restype = C.c_double
         L.orc_gamma.argtypes = [C.c_double, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_amm_stats.argtypes = [C.POINTER(C.c_int64)]
+        L.orc_amm_stats_reset.argtypes = []
         self.L = L
 
     def _ir(self, model):
@@ -120,6 +122,15 @@ class Oracle:
                                               xx.ctypes.data_as(dp), g.ctypes.data_as(dp))
             return lp, g
         return self.L.orc_block_logpdf(C.byref(spec), ptrs, ns, v.ctypes.data_as(dp), block, xx.ctypes.data_as(dp))
+
+    def amm_stats(self, reset=False):
+        """Per-block AMM counters since the last reset: (cholfact calls, rank == n, rank sum)."""
+        v = (C.c_int64 * (8 * 3))()
+        self.L.orc_amm_stats(v)
+        if reset:
+            self.L.orc_amm_stats_reset()
+        return {b: {"updates": v[3 * b], "full_rank": v[3 * b + 1], "rank_sum": v[3 * b + 2]}
+                for b in range(8) if v[3 * b]}
 
     def pchol(self, S):
         d = S.shape[0]

@@ -42,8 +42,10 @@ def _run(mamba, m, init, windows, seed=5, generic=False, model_burnin=None):
 
 
 @pytest.mark.parametrize("name", sorted(SCHEMES))
-def test_line_amm_quad_vs_generic_4096(mamba, name):
-    """Full configs[1] size; 300 iterations = 4 launches + a ragged one; adaptive switch at m > 2d."""
+def test_line_amm_quad_vs_generic_4096(mamba, name, monkeypatch):
+    """Full configs[1] size; 300 iterations at 64 per launch = 4 launches + a ragged one (the
+    default is 256 per launch); adaptive switch at m > 2d."""
+    monkeypatch.setenv("MMB_ITERS_PER_LAUNCH", "64")
     m = _model(mamba, name)
     init = mamba.model.line_init_matrix(4096, seed=11)
     fq, vq, tq = _run(mamba, m, init, [(300, 100, 2)], model_burnin=150)
@@ -68,13 +70,15 @@ def test_line_amm_quad_vs_oracle_4096(mamba, oracle, name):
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
 
 
-def test_line_amm_quad_window_splits(mamba):
+def test_line_amm_quad_window_splits(mamba, monkeypatch):
     """Register-resident tune state is written back at every launch end: windows of 1, 63, 65
-    and 71 iterations (launch boundaries inside and across windows) equal one 200-iteration run,
-    and a host round trip of values + tune (set_values / set_tune) in between changes nothing."""
+    and 71 iterations at 16 iterations per launch (launch boundaries inside and across windows)
+    equal one 200-iteration run at the default 256 per launch (a single ragged launch), and a
+    host round trip of values + tune (set_values / set_tune) in between changes nothing."""
     m = _model(mamba, "amm")
     init = mamba.model.line_init_matrix(4096, seed=13)
     full, vf, tf = _run(mamba, m, init, [(200, 0, 1)])
+    monkeypatch.setenv("MMB_ITERS_PER_LAUNCH", "16")
     eng = mamba.Engine(m)
     eng.init_chains(init, seed=5)
     parts = [eng.run(1), eng.run(63), eng.run(65)]

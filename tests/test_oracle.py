@@ -77,6 +77,21 @@ def test_line_gradient_golden(mamba, oracle):
         assert g2[2] == pytest.approx(c["grad_ls2"], rel=1e-10)
 
 
+def test_line_analytic_gradient_follows_block_order(mamba, oracle):
+    """dtype="analytic" on blocks that list s2 first or hold s2 alone: the gradient
+    is in the block's element order (unlist order, simulation.jl:110-163) -- [s2, beta] gives
+    (d/dlog s2, d/dbeta0, d/dbeta1), [s2] gives d/dlog s2 -- and equals the golden partials."""
+    m = line_model(mamba, [mamba.NUTS(["s2", "beta"], dtype="analytic"), mamba.NUTS("s2", dtype="analytic"),
+                           mamba.NUTS("beta", dtype="analytic")])
+    for c in load("logpdf.json")["line_grad"]:
+        v = c["vals"]
+        _, g = oracle.block_logpdf(m, v, 0, [np.log(v[2]), v[0], v[1]], grad=True)
+        assert g[0] == pytest.approx(c["grad_ls2"], rel=1e-10)
+        np.testing.assert_allclose(g[1:], c["grad_beta"], rtol=1e-11)
+        _, g = oracle.block_logpdf(m, v, 1, [np.log(v[2])], grad=True)
+        assert g[0] == pytest.approx(c["grad_ls2"], rel=1e-10)
+
+
 def test_line_forward_difference_gradient(mamba, oracle):
     """The reference's default gradient (dtype=:forward, simulation.jl:47-51 -> Calculus
     finite_difference!): g_i = (f(x + e_i eps_i) - f(x)) / eps_i, eps_i = sqrt(eps()) * max(1, |x_i|),
@@ -320,3 +335,53 @@ def test_logistic_hmc_mala_posterior_laplace(mamba, oracle, scheme):
     mean = d.mean(axis=(0, 2))
     assert np.all(np.abs(mean - b) < 0.15 * sd), (mean, b, sd)
     assert np.all(np.abs(d.std(axis=(0, 2)) / sd - 1) < 0.1), (d.std(axis=(0, 2)), sd)
+
+
+def test_rats_amm_alias_leaves_first_accepted_chains_without_factor(mamba, oracle):
+    """Mechanism behind the config-3 full-rank fraction.  setadapt! aliases
+    tune.Mv to the variate (/root/reference/src/samplers/amm.jl:102: tune.Mv = v), so the first
+    adaptive update computes Mv = p v1 + (1-p) v1 = v1 while Mvv = (v0 v0' + v1 v1') / 2
+    (amm.jl:84-85).  When that first proposal was accepted (v1 != v0), Mvv - Mv Mv' carries the
+    indefinite term (v0 v0' - v1 v1') / 2 at the scale |v| |v1 - v0| (alpha ~ 240), which the
+    running averages shrink only like 2 / (m + 1); dpstf2 then stops early every update,
+    rank(F) < n, and SigmaLm keeps setadapt!'s zeros (amm.jl:88-90, 104).  Pinned on the bench's
+    own inits (rats_init_ls(16384, seed=1000)[:1024]) at m = 400 and m = 5000: every alpha chain
+    whose first AMM proposal was accepted has no valid factor, every first-rejected one has one;
+    beta (Sigma = 0.01 I, smaller |v|) the same at m = 400."""
+    m = rats_model(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_ls(16384, seed=1000)[:1024]
+    st = oracle.new_state(m, init)
+    v0 = st["values"].copy()
+    oracle.run(m, st, 1, seed=7, nthreads=8, draws=False)
+    # value layout: s2_c | alpha[30] | mu_alpha | s2_alpha | beta[30] | mu_beta | s2_beta
+    acc_a = (st["values"][:, 1:31] != v0[:, 1:31]).any(1)
+    acc_b = (st["values"][:, 33:63] != v0[:, 33:63]).any(1)
+    assert 0.3 < acc_a.mean() < 0.7 and 0.2 < acc_b.mean() < 0.6
+    d, T = 30, 465
+    tl = 4 + 2 * d + 2 * T  # oracle AMM tune: adapt, m, valid, alias, Mv[d], Mvv[T], Ls[T], piv[d]
+    oracle.run(m, st, 399, seed=7, nthreads=8, draws=False)
+    t = st["tune"]
+    assert t[0, 1] == 400 and t[0, tl + 1] == 400
+    va, vb = t[:, 2] != 0, t[:, tl + 2] != 0
+    assert not va[acc_a].any() and va[~acc_a].all()
+    assert not vb[acc_b].any() and vb[~acc_b].all()
+    # the moment matrix itself: indefinite for every first-accepted alpha chain, PSD (up to
+    # rounding) for the first-rejected ones
+    ii, kk = np.tril_indices(d)
+    tri = ii * (ii + 1) // 2 + kk
+    lam = []
+    for c in range(0, 1024, 8):
+        Mv, Mvv = t[c, 4:4 + d], t[c, 4 + d:4 + d + T]
+        S = np.zeros((d, d))
+        S[ii, kk] = Mvv[tri] - Mv[kk] * Mv[ii]
+        S[kk, ii] = S[ii, kk]
+        lam.append(np.linalg.eigvalsh(S)[0])
+    lam = np.array(lam)
+    assert (lam[acc_a[::8]] < -1.0).all()
+    assert (lam[~acc_a[::8]] > -1e-6).all()
+    oracle.run(m, st, 4600, seed=7, nthreads=8, draws=False)
+    t = st["tune"]
+    assert t[0, 1] == 5000
+    va, vb = t[:, 2] != 0, t[:, tl + 2] != 0
+    assert not va[acc_a].any() and va[~acc_a].all()
+    assert vb[acc_b].mean() < 0.01 and vb[~acc_b].all()
