@@ -218,9 +218,12 @@ def setup_workload(mb, args, rank):
     data, _ = mb.model.logistic_data(10000, 50)
     model = mb.logistic(10000, 50, 10.0)
     model.setinputs(data)
-    model.setsamplers([mb.NUTS("beta")])
+    # the logistic kernel's gradient is the analytic one, asked for explicitly: the reference's
+    # default dtype=:forward (Calculus) is refused by mmb_create (MMB_E_UNSUPPORTED)
+    model.setsamplers([mb.NUTS("beta", dtype="analytic")])
     init = np.random.default_rng(1000 + rank).normal(0.0, 0.1, (K, 50))
-    return model, init, "logistic N=10000 p=50 NUTS (BASELINE configs[3])", {"thin": 1}, "f64"
+    return (model, init, "logistic N=10000 p=50 NUTS (BASELINE configs[3]), analytic gradient (dtype=:analytic; "
+            "the reference default :forward is refused by this kernel)", {"thin": 1}, "f64")
 
 
 def amm_window(model, before, after):

@@ -26,7 +26,14 @@ const MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC = Int32(1), Int32(2), I
 const MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE = Int32(1), Int32(2), Int32(3), Int32(4)
 const MMB_SAMPLER_GIBBS, MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = Int32(5), Int32(6), Int32(7)
 const MMB_ADAPT = Dict(:all => Int32(0), :burnin => Int32(1), :none => Int32(2))
-const MMB_GRAD_DEFAULT = Int32(0)   # mmb_gradient: the model's default (:forward on line / node IR)
+const MMB_GRAD_DEFAULT, MMB_GRAD_FORWARD, MMB_GRAD_ANALYTIC = Int32(0), Int32(1), Int32(2)  # mmb_gradient
+# dtype of NUTS / HMC / MALA -> mmb_gradient.  :forward is the reference's default (Calculus,
+# simulation.jl:47-51), passed as MMB_GRAD_FORWARD: the logistic kernel has no forward-difference
+# gradient and mmb_create answers MMB_E_UNSUPPORTED, so that model keeps the Julia path instead of
+# silently getting another gradient.  :analytic is MambaHIP's opt-in to the hand-derived gradient
+# (line, logistic); the Julia-side Sampler is built with :forward (Calculus has no :analytic).
+const MMB_GRAD = Dict(:forward => MMB_GRAD_FORWARD, :analytic => MMB_GRAD_ANALYTIC)
+julia_dtype(dtype::Symbol) = dtype == :analytic ? :forward : dtype
 const MMB_COMM_ID_BYTES = 128
 
 # ---- structs (layout-checked against the header by tests/test_abi.py on the Python side) ----
@@ -145,17 +152,17 @@ AMM(params, Sigma::Matrix; adapt::Symbol=:all, args...) =                    # a
   register(Mamba.AMM(params, Sigma; adapt=adapt, args...), MMB_SAMPLER_AMM, (Sigma,),
            Any[(:adapt, adapt), args...])
 NUTS(params; dtype::Symbol=:forward, args...) =                              # nuts.jl:47-56
-  register(Mamba.NUTS(params; dtype=dtype, args...), MMB_SAMPLER_NUTS, (),
+  register(Mamba.NUTS(params; dtype=julia_dtype(dtype), args...), MMB_SAMPLER_NUTS, (),
            Any[(:dtype, dtype), args...])
 Slice(params, width, F::Type=Multivariate; transform::Bool=false) =          # slice.jl:47-58
   register(Mamba.Slice(params, width, F; transform=transform), MMB_SAMPLER_SLICE, (width, F),
            Any[(:transform, transform)])
 HMC(params, epsilon::Real, L::Integer, pargs...; dtype::Symbol=:forward) =   # hmc.jl:47-65
-  register(Mamba.HMC(params, epsilon, L, pargs...; dtype=dtype), MMB_SAMPLER_HMC, (epsilon, L, pargs...),
-           Any[(:dtype, dtype)])
+  register(Mamba.HMC(params, epsilon, L, pargs...; dtype=julia_dtype(dtype)), MMB_SAMPLER_HMC,
+           (epsilon, L, pargs...), Any[(:dtype, dtype)])
 MALA(params, epsilon::Real, pargs...; dtype::Symbol=:forward) =              # mala.jl:43-58
-  register(Mamba.MALA(params, epsilon, pargs...; dtype=dtype), MMB_SAMPLER_MALA, (epsilon, pargs...),
-           Any[(:dtype, dtype)])
+  register(Mamba.MALA(params, epsilon, pargs...; dtype=julia_dtype(dtype)), MMB_SAMPLER_MALA,
+           (epsilon, pargs...), Any[(:dtype, dtype)])
 
 # tune type each constructor creates (amwg.jl:60, amm.jl:58, nuts.jl:55, slice.jl:57,
 # hmc.jl:64, mala.jl:59): a registered block must still carry it
@@ -189,9 +196,11 @@ function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::In
   r = registered(s)
   r === nothing && return nothing                   # an arbitrary user closure: keep the Julia path
   isa(s.tune, TUNE_OF[r.kind]) || return nothing
+  grad = get(MMB_GRAD, kwarg(r, :dtype, :forward), Int32(-1))
   blk(adapt_, form, transform, batchsize, target, beta, scale, tun, eps, L) =
     BlockSpec(r.kind, nnodes, nodes, adapt_, form, transform, batchsize, target, beta, scale, dim,
-              length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L, MMB_GRAD_DEFAULT)
+              length(tun), isempty(tun) ? C_NULL : pointer(tun), eps, L,
+              r.kind in (MMB_SAMPLER_NUTS, MMB_SAMPLER_HMC, MMB_SAMPLER_MALA) ? grad : MMB_GRAD_DEFAULT)
   adapt = MMB_ADAPT[kwarg(r, :adapt, :none)]
   if r.kind == MMB_SAMPLER_GIBBS
     return blk(MMB_ADAPT[:none], 0, 0, 0, 0.0, 0.0, 0.0, Float64[], 0.0, 0)
@@ -204,9 +213,9 @@ function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::In
     size(r.pargs[1], 1) == dim || throw(ArgumentError("Sigma dimension differs from variate length $dim"))
     return blk(adapt, 0, 1, 0, 0.0, kwarg(r, :beta, 0.05), kwarg(r, :scale, 2.38), Sig, 0.0, 0)
   elseif r.kind == MMB_SAMPLER_NUTS                                            # nuts.jl:5-39
-    # the device differentiates with :forward differences (Calculus, simulation.jl:47-51) or, on
-    # the logistic kernel, analytically; any other dtype keeps the Julia path
-    kwarg(r, :dtype, :forward) == :forward || return nothing
+    # :forward (Calculus forward differences, simulation.jl:47-51; refused by the logistic kernel:
+    # MMB_E_UNSUPPORTED -> Julia path) or :analytic (MMB_GRAD); any other dtype keeps the Julia path
+    grad < 0 && return nothing
     return blk(MMB_ADAPT[:burnin], 0, 1, 0, kwarg(r, :target, 0.6), 0.0, 0.0, Float64[], 0.0, 0)
   elseif r.kind == MMB_SAMPLER_SLICE                                           # slice.jl:7-26
     w = fillvec(r.pargs[1], dim); push!(keep, w)
@@ -214,7 +223,7 @@ function block_spec(s::Sampler, nodes::NTuple{4,Int32}, nnodes::Integer, dim::In
     form = r.pargs[2] == Univariate ? Int32(1) : Int32(0)
     return blk(MMB_ADAPT[:none], form, Int32(kwarg(r, :transform, false)), 0, 0.0, 0.0, 0.0, w, 0.0, 0)
   else                                                                         # hmc.jl:5-32, mala.jl:5-30
-    kwarg(r, :dtype, :forward) == :forward || return nothing
+    grad < 0 && return nothing
     hmc = r.kind == MMB_SAMPLER_HMC
     nS = hmc ? 3 : 2                                  # (epsilon, L[, Sigma]) / (epsilon[, Sigma])
     S = length(r.pargs) >= nS ? vec(Float64[r.pargs[nS]...]) : Float64[]; push!(keep, S)

@@ -20,8 +20,18 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
 
 
+def _deps_mtime(src):
+    """Newest of the source and every header it may include (csrc/*.h, include/*.h)."""
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    inc = os.path.join(ROOT, "include")
+    hdrs += [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h")]
+    return max(os.path.getmtime(x) for x in [os.path.join(CSRC, src), *hdrs, __file__])
+
+
 def _compile(src, objdir, defines=()):
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
+    if os.path.exists(obj) and os.path.getmtime(obj) > _deps_mtime(src) and not os.environ.get("MMB_REBUILD"):
+        return obj  # up to date (same flags: the object directory is per define set)
     cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -322,8 +322,16 @@ static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int d
     // model supports them (line, node IR), the analytic gradient on line and logistic
     if (s.sampler == MMB_SAMPLER_NUTS || s.sampler == MMB_SAMPLER_HMC || s.sampler == MMB_SAMPLER_MALA) {
       const int gr = s.gradient;
-      const bool ok = gr == MMB_GRAD_DEFAULT ||
-                      (gr == MMB_GRAD_FORWARD && e->model != MMB_MODEL_LOGISTIC) ||
+      if (gr == MMB_GRAD_FORWARD && e->model == MMB_MODEL_LOGISTIC) {
+        // the reference's default dtype=:forward (Calculus forward differences, simulation.jl:47-51)
+        // is not on the logistic kernel: refused explicitly (the caller keeps the Julia path or
+        // asks for the analytic gradient), never silently replaced
+        delete e;
+        return fail(nullptr, MMB_E_UNSUPPORTED,
+                    "block %d: logistic has no forward-difference gradient kernel (dtype=:forward); "
+                    "use dtype=:analytic (MMB_GRAD_ANALYTIC) for the batched analytic gradient", b);
+      }
+      const bool ok = gr == MMB_GRAD_DEFAULT || gr == MMB_GRAD_FORWARD ||
                       (gr == MMB_GRAD_ANALYTIC && e->model != MMB_MODEL_IR);
       if (!ok) {
         delete e;

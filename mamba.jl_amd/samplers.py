@@ -95,12 +95,14 @@ def NUTS(params, dtype="forward", target=0.6):
 
 def _dtype(dtype):
     """logpdfgrad! scheme (sampler.jl:97-111 -> simulation.jl:47-51, Calculus): "forward" (the
-    reference's default) -> MMB_GRAD_DEFAULT: forward differences on line and the node IR, the
-    analytic gradient kernel on logistic (configs[3]); "analytic" -> the hand-derived gradient
-    (line, logistic).  Calculus' :central / :complex are not on the device."""
+    reference's default) -> MMB_GRAD_FORWARD: Calculus forward differences (line, node IR; the
+    logistic kernel has none: mmb_create refuses it with MMB_E_UNSUPPORTED, so a reference-default
+    NUTS(:beta) on logistic is never silently given another gradient); "analytic" -> the
+    hand-derived gradient (line, logistic: the config-4 kernel's batched MFMA gradient).
+    Calculus' :central / :complex are not on the device."""
     d = str(dtype).lstrip(":")
     if d == "forward":
-        return abi.MMB_GRAD_DEFAULT
+        return abi.MMB_GRAD_FORWARD
     if d == "analytic":
         return abi.MMB_GRAD_ANALYTIC
     if d in ("central", "complex"):

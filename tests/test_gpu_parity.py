@@ -249,7 +249,7 @@ def logistic(mamba, nobs, ncoef, scheme=None):
     data, bt = mamba.model.logistic_data(nobs, ncoef)
     m = mamba.logistic(nobs, ncoef, 10.0)
     m.setinputs(data)
-    return m.setsamplers(scheme or [mamba.NUTS("beta")]), bt
+    return m.setsamplers(scheme or [mamba.NUTS("beta", dtype="analytic")]), bt
 
 
 def _spd(p, seed, a, b):
@@ -258,10 +258,10 @@ def _spd(p, seed, a, b):
 
 
 LOGISTIC_GRAD_SCHEMES = {
-    "hmc": lambda M, p: [M.HMC("beta", 0.01, 7)],
-    "hmc_sigma": lambda M, p: [M.HMC("beta", 0.01, 4, _spd(p, 1, 0.2, 1.0))],   # near I (unit-mass leapfrog)
-    "mala": lambda M, p: [M.MALA("beta", 2e-4)],
-    "mala_sigma": lambda M, p: [M.MALA("beta", 0.5, _spd(p, 2, 1e-3, 1e-4))],
+    "hmc": lambda M, p: [M.HMC("beta", 0.01, 7, dtype="analytic")],
+    "hmc_sigma": lambda M, p: [M.HMC("beta", 0.01, 4, _spd(p, 1, 0.2, 1.0), dtype="analytic")],  # near I
+    "mala": lambda M, p: [M.MALA("beta", 2e-4, dtype="analytic")],
+    "mala_sigma": lambda M, p: [M.MALA("beta", 0.5, _spd(p, 2, 1e-3, 1e-4), dtype="analytic")],
 }
 
 
@@ -407,7 +407,7 @@ def test_checkpoint_file_resume_line(mamba, tmp_path, name):
 def test_checkpoint_file_resume_logistic(mamba, tmp_path, name):
     """Logistic (config 4 at N=1000): the resumable NUTS / HMC machines hold no state across
     iteration boundaries beyond values + tune, so a file checkpoint resumes exactly."""
-    sch = (lambda: [mamba.NUTS("beta")]) if name == "nuts" else (lambda: LOGISTIC_GRAD_SCHEMES["hmc"](mamba, 50))
+    sch = (lambda: [mamba.NUTS("beta", dtype="analytic")]) if name == "nuts" else (lambda: LOGISTIC_GRAD_SCHEMES["hmc"](mamba, 50))
     K = 100
     init = np.random.default_rng(8).normal(0.0, 0.1, (K, 50))
     m, _ = logistic(mamba, 1000, 50, sch())
@@ -490,7 +490,7 @@ def test_logistic_nuts_parity_full(mamba, oracle):
 @pytest.mark.parametrize("p", [53, 64])
 def test_logistic_wide_parity(mamba, oracle, p):
     """53 <= p <= MMB_LG_DV: the 16-k-step first GEMM (coefficients 52..63 are part of eta)."""
-    for sch in ([mamba.NUTS("beta")], [mamba.HMC("beta", 0.01, 5)]):
+    for sch in ([mamba.NUTS("beta", dtype="analytic")], [mamba.HMC("beta", 0.01, 5, dtype="analytic")]):
         m, _ = logistic(mamba, 1000, p, sch)
         K = 40
         init = np.random.default_rng(p).normal(0.0, 0.1, (K, p))
@@ -512,7 +512,7 @@ def test_logistic_group_mode_parity(mamba, oracle):
     np.testing.assert_array_equal(dg, do)
     np.testing.assert_array_equal(eng.values(), st["values"])
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
-    m, _ = logistic(mamba, 10000, 50, [mamba.HMC("beta", 0.005, 2)])
+    m, _ = logistic(mamba, 10000, 50, [mamba.HMC("beta", 0.005, 2, dtype="analytic")])
     K = 1024
     init = np.random.default_rng(32).normal(0.0, 0.1, (K, 50))
     eng, dg, st, do = both(mamba, oracle, m, init, 2, 0, 1)
@@ -631,13 +631,14 @@ def test_rats_scale_total_on_one_gpu(mamba, oracle):
 
 def test_gradient_choice_validated(mamba):
     """mmb_gradient (include/mamba_hip.h): forward differences are not available on the logistic
-    kernel, the analytic gradient not on the node IR; both are refused at mmb_create."""
+    kernel, the analytic gradient not on the node IR; both are refused at mmb_create.  The
+    reference's default NUTS(:beta) (dtype=:forward) on logistic is refused, never silently
+    given the analytic gradient."""
     A = mamba.abi
     m = mamba.logistic(200, 5, 10.0)
-    s = mamba.NUTS("beta")
-    s.gradient = A.MMB_GRAD_FORWARD
-    m.setsamplers([s])
-    with pytest.raises(RuntimeError, match="gradient"):
+    m.setsamplers([mamba.NUTS("beta")])
+    assert m.samplers[0].gradient == A.MMB_GRAD_FORWARD
+    with pytest.raises(RuntimeError, match="forward-difference"):
         mamba.Engine(m)
     ir = mamba.ir
     mi = ir.seeds_model().setinputs(ir.SEEDS)

@@ -59,7 +59,7 @@ def test_logistic_logpdf_and_gradient_golden(mamba, oracle):
     dd = g["logistic_data"]
     m = mamba.logistic(dd["N"], dd["p"], dd["sd"])
     m.setinputs({"X": dd["X"], "y": dd["y"]})
-    m.setsamplers([mamba.NUTS("beta")])
+    m.setsamplers([mamba.NUTS("beta", dtype="analytic")])
     for c in g["logistic"]:
         lp, gr = oracle.block_logpdf(m, c["beta"], 0, c["beta"], grad=True)
         assert lp == pytest.approx(c["lp"], rel=1e-11)
@@ -299,7 +299,7 @@ def test_logistic_nuts_posterior_laplace(mamba, oracle):
     X, y = data["X"], data["y"]
     m = mamba.logistic(N, p, 10.0)
     m.setinputs(data)
-    m.setsamplers([mamba.NUTS("beta")])
+    m.setsamplers([mamba.NUTS("beta", dtype="analytic")])
     b = np.zeros(p)
     for _ in range(50):                                   # Newton for the MAP
         mu = 1.0 / (1.0 + np.exp(-(X @ b)))
@@ -322,7 +322,8 @@ def test_logistic_hmc_mala_posterior_laplace(mamba, oracle, scheme):
     X, y = data["X"], data["y"]
     m = mamba.logistic(N, p, 10.0)
     m.setinputs(data)
-    m.setsamplers([mamba.HMC("beta", 0.02, 8) if scheme == "hmc" else mamba.MALA("beta", 1.5e-3)])
+    m.setsamplers([mamba.HMC("beta", 0.02, 8, dtype="analytic") if scheme == "hmc"
+                   else mamba.MALA("beta", 1.5e-3, dtype="analytic")])
     b = np.zeros(p)
     for _ in range(50):
         mu = 1.0 / (1.0 + np.exp(-(X @ b)))
