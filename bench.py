@@ -485,6 +485,10 @@ def main():
             out["config"]["amm_adapt"] = "all"
     if amm_timed:
         out["config"]["amm"] = amm_timed
+    if args.workload.endswith("_ir"):
+        # node IR: the specialised kernel (mmb_create_ir -> hipRTC, csrc/ir_jit.cpp) or the interpreter
+        jit, info = eng.ir_jit()
+        out["config"]["ir_kernel"] = {"specialised": jit, "info": info}
     if nuts_timed is not None:
         out["nuts"] = nuts_timed
     if psrf is not None:

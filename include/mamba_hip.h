@@ -23,8 +23,20 @@
 #ifndef MAMBA_HIP_H
 #define MAMBA_HIP_H
 
+#if !defined(__HIPCC_RTC__)
 #include <stddef.h>
 #include <stdint.h>
+#else  /* hipRTC (node-IR specialisation): fixed-width types from its runtime header */
+typedef __hip_internal::int8_t int8_t;
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::int16_t int16_t;
+typedef __hip_internal::uint16_t uint16_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __UINTPTR_TYPE__ uintptr_t;
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -325,6 +337,19 @@ int mmb_grad_evals(mmb_engine* e, int64_t* n);
  * reference's unbounded doubling loop (nuts.jl:106-125) would have continued, out[2] = sum of
  * final tree depths j.  out[1] == 0 means the cap never changed a draw. */
 int mmb_nuts_stats(mmb_engine* e, int64_t out[3]);
+/* Node-IR kernel specialisation.  mmb_create_ir writes the lowered model as
+ * HIP source -- node log densities (dependent.jl:207-213 -> distributionstruct.jl:136-168) and
+ * block logpdf! term lists (simulation.jl:77-90) as straight-line code -- and compiles it with
+ * hipRTC (code objects cached by source hash: MMB_JIT_CACHE, else <library dir>/jit), replacing
+ * the per-op interpreter; the same operations in the same order, so results are bit-identical.
+ * On any failure, or with MMB_IR_JIT=0, the interpreter kernel runs.
+ * mmb_ir_jit_info: 1 if the engine runs the specialised kernel, 0 if the interpreter; `buf`
+ * receives the reason / cache status.  mmb_ir_jit_prebuild: validate and compile into the cache
+ * without a device (build step).  mmb_ir_jit_source_text: the generated source (returns its
+ * length; copies up to n - 1 bytes). */
+int mmb_ir_jit_info(const mmb_engine* e, char* buf, int64_t n);
+int mmb_ir_jit_prebuild(const mmb_model_spec* spec, const mmb_ir_model* ir, char* info, int64_t n);
+int mmb_ir_jit_source_text(const mmb_model_spec* spec, const mmb_ir_model* ir, char* buf, int64_t n);
 /* AMM factorization statistics since mmb_init_chains, per sampling block b (zero rows for
  * non-AMM blocks), summed over the engine's chains: out[b*MMB_AMM_STATS + i] =
  *   i = 0  adaptive updates, i.e. cholfact(Hermitian(Sigma), Val{true}) calls (amm.jl:81-87)

@@ -115,6 +115,9 @@ def _declare(lib):
         "mmb_grad_evals": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_nuts_stats": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_amm_stats": (C.c_int, [P, C.POINTER(I64)]),
+        "mmb_ir_jit_info": (C.c_int, [P, C.c_char_p, I64]),
+        "mmb_ir_jit_prebuild": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_char_p, I64]),
+        "mmb_ir_jit_source_text": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_char_p, I64]),
         "mmb_comm_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "mmb_comm_init": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(P)]),
         "mmb_range_allreduce": (C.c_int, [P, D]),

@@ -7,14 +7,33 @@
 // Group-uniform control flow only; group reductions are xor-butterflies inside
 // the G-aligned lane group, so every lane of a group ends with the same value.
 #pragma once
+#if !defined(__HIPCC_RTC__)  // hipRTC (the node-IR JIT, engine.cpp) brings its own runtime header
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "../../include/mamba_hip.h"
 #include "mmb_math.h"
 #include "ir_math.h"
 
 #define MMB_MAXB MMB_MAX_BLOCKS
+
+// lane's bit of a wave mask.  hipRTC's compiler (the one torch bundles) lacks the wave64 builtin;
+// there the bit is extracted by the lane id (node-IR specialised kernels only).
+__device__ __forceinline__ bool mmb_inverse_ballot(uint64_t m) {
+#if defined(__HIPCC_RTC__)
+  return ((m >> (threadIdx.x & 63)) & 1ull) != 0ull;
+#else
+  return __builtin_amdgcn_inverse_ballot_w64(m);
+#endif
+}
+
+// compile-time bool tag (a std::integral_constant without <type_traits>, which hipRTC lacks)
+template <bool B>
+struct mmb_bc {
+  static constexpr bool value = B;
+  constexpr operator bool() const { return B; }
+};
 
 // Correctly rounded sqrt(x) and 1/y for operands well inside the normal range, without the
 // range handling of the generic sequences.  For x in [2^-700, 2^700] these are the very

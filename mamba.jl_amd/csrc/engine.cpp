@@ -21,6 +21,7 @@
 #include "nuts.h"
 #include "logistic.h"
 #include "ir.h"
+#include "ir_jit.h"
 
 #include <rccl/rccl.h>
 
@@ -101,6 +102,10 @@ struct mmb_engine {
   int32_t *d_ir_code = nullptr, *d_ir_mon = nullptr;
   double *d_ir_const = nullptr, *d_ir_pool = nullptr;
   mmb_ir_block* d_ir_blocks = nullptr;
+  // node IR specialised kernel (ir_jit.cpp): null when the interpreter kernel runs
+  hipModule_t jit_mod = nullptr;
+  hipFunction_t jit_fn = nullptr;
+  std::string jit_info;
   // timing
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> evpool;  // 2 per launch when time_kernels
@@ -501,8 +506,7 @@ static int ir_check_expr(const mmb_ir_model* ir, int pc, int len, int* depth) {
   return -1;
 }
 
-int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out) {
-  if (!spec || !ir || !out) return fail(nullptr, MMB_E_ARG, "null argument");
+static int ir_validate(const mmb_model_spec* spec, const mmb_ir_model* ir) {
   if (spec->model != MMB_MODEL_IR) return fail(nullptr, MMB_E_ARG, "spec->model must be MMB_MODEL_IR");
   if (ir->nvalues < 1 || ir->nvalues > MMB_IR_MAX_VALUES)
     return fail(nullptr, MMB_E_UNSUPPORTED, "node IR: 1 <= nvalues <= %d", MMB_IR_MAX_VALUES);
@@ -550,7 +554,95 @@ int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device
       if (B.term[t] < 0 || B.term[t] >= ir->nnodes || ir->nodes[B.term[t]].family == MMB_IR_LOGICAL)
         return fail(nullptr, MMB_E_ARG, "node IR: block %d term %d invalid", b, t);
   }
-  return create_impl(spec, ir, device, out);
+  return 0;
+}
+
+// Sampler kinds of the scheme and its widest AMM block (the specialised kernel's parameters)
+static void ir_jit_params(const mmb_model_spec* spec, const mmb_ir_model* ir, unsigned* kinds, int* dmax) {
+  *kinds = 0;
+  *dmax = 0;
+  for (int b = 0; b < spec->nblocks; ++b) {
+    const mmb_block_spec& s = spec->blocks[b];
+    *kinds |= 1u << s.sampler;
+    int d = 0;
+    for (int a = 0; a < s.nnodes; ++a) d += std::max(0, node_dim(*spec, ir, s.nodes[a], nullptr));
+    if (s.sampler == MMB_SAMPLER_AMM) *dmax = std::max(*dmax, d);
+  }
+  if (*dmax == 0) *dmax = Mdl<MMB_MODEL_IR>::DMAX;  // no AMM block: the factorization is not compiled
+}
+
+// The specialised kernel of a node-IR engine (ir_jit.cpp); on any failure the interpreter
+// kernel runs (jit_info says why).  MMB_IR_JIT=0 selects the interpreter.
+static void ir_jit_setup(mmb_engine* e, const mmb_model_spec* spec, const mmb_ir_model* ir) {
+  const char* env = std::getenv("MMB_IR_JIT");
+  if (env && std::string(env) == "0") {
+    e->jit_info = "interpreter (MMB_IR_JIT=0)";
+    return;
+  }
+  unsigned kinds = 0;
+  int dmax = 0;
+  ir_jit_params(spec, ir, &kinds, &dmax);
+  std::vector<char> code;
+  std::string info;
+  if (mmb_ir_jit_obtain(mmb_ir_jit_source(*spec, *ir, kinds, dmax), &code, &info)) {
+    e->jit_info = "interpreter (specialisation failed: " + info + ")";
+    return;
+  }
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  hipError_t st = hipSetDevice(e->device);
+  if (st == hipSuccess) st = hipModuleLoadData(&mod, code.data());
+  if (st == hipSuccess) st = hipModuleGetFunction(&fn, mod, "mmb_ir_jit_kernel");
+  if (st != hipSuccess) {
+    if (mod) (void)hipModuleUnload(mod);
+    e->jit_info = std::string("interpreter (module load failed: ") + hipGetErrorString(st) + ")";
+    return;
+  }
+  e->jit_mod = mod;
+  e->jit_fn = fn;
+  e->jit_info = "specialised kernel (" + info + ")";
+}
+
+int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out) {
+  if (!spec || !ir || !out) return fail(nullptr, MMB_E_ARG, "null argument");
+  int rc = ir_validate(spec, ir);
+  if (rc) return rc;
+  rc = create_impl(spec, ir, device, out);
+  if (rc) return rc;
+  ir_jit_setup(*out, spec, ir);
+  return 0;
+}
+
+int mmb_ir_jit_prebuild(const mmb_model_spec* spec, const mmb_ir_model* ir, char* info, int64_t n) {
+  if (!spec || !ir) return fail(nullptr, MMB_E_ARG, "null argument");
+  int rc = ir_validate(spec, ir);
+  if (rc) return rc;
+  unsigned kinds = 0;
+  int dmax = 0;
+  ir_jit_params(spec, ir, &kinds, &dmax);
+  std::vector<char> code;
+  std::string msg;
+  rc = mmb_ir_jit_obtain(mmb_ir_jit_source(*spec, *ir, kinds, dmax), &code, &msg);
+  if (info && n > 0) snprintf(info, (size_t)n, "%s", msg.c_str());
+  return rc ? fail(nullptr, MMB_E_UNSUPPORTED, "%s", msg.c_str()) : 0;
+}
+
+int mmb_ir_jit_source_text(const mmb_model_spec* spec, const mmb_ir_model* ir, char* buf, int64_t n) {
+  if (!spec || !ir) return fail(nullptr, MMB_E_ARG, "null argument");
+  int rc = ir_validate(spec, ir);
+  if (rc) return rc;
+  unsigned kinds = 0;
+  int dmax = 0;
+  ir_jit_params(spec, ir, &kinds, &dmax);
+  const std::string src = mmb_ir_jit_source(*spec, *ir, kinds, dmax);
+  if (buf && n > 0) snprintf(buf, (size_t)n, "%s", src.c_str());
+  return (int)std::min<size_t>(src.size(), (size_t)INT32_MAX);
+}
+
+int mmb_ir_jit_info(const mmb_engine* e, char* buf, int64_t n) {
+  if (!e) return fail(nullptr, MMB_E_ARG, "null argument");
+  if (buf && n > 0) snprintf(buf, (size_t)n, "%s", e->model == MMB_MODEL_IR ? e->jit_info.c_str() : "not a node-IR engine");
+  return e->jit_fn ? 1 : 0;
 }
 
 static void free_dev(mmb_engine* e) {
@@ -624,6 +716,7 @@ void mmb_destroy(mmb_engine* e) {
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->jit_mod) (void)hipModuleUnload(e->jit_mod);
   delete e;
 }
 
@@ -1116,7 +1209,16 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
     A.iter0 = it0 + done;
     A.n_iters = w;
     if (a->time_kernels) HIPCHK(e, hipEventRecord(e->evpool[2 * li], e->stream));
-    hipError_t st = mmb_launch_sweep(e->model, e->kinds, A, e->stream);
+    hipError_t st;
+    if (e->jit_fn) {  // node IR, specialised kernel: the interpreter's launch shape (4 chains / 128 threads)
+      const int per_block = 128 / Mdl<MMB_MODEL_IR>::G;
+      const unsigned grid = (unsigned)((A.K + per_block - 1) / per_block);
+      const size_t lds = (size_t)per_block * Mdl<MMB_MODEL_IR>::lds_stride(A) * sizeof(double);
+      void* args[] = {(void*)&A};
+      st = hipModuleLaunchKernel(e->jit_fn, grid, 1, 1, 128, 1, 1, (unsigned)lds, e->stream, args, nullptr);
+    } else {
+      st = mmb_launch_sweep(e->model, e->kinds, A, e->stream);
+    }
     if (st != hipSuccess) return fail(e, MMB_E_HIP, "sweep launch: %s", hipGetErrorString(st));
     if (a->time_kernels) HIPCHK(e, hipEventRecord(e->evpool[2 * li + 1], e->stream));
     e->launches += 1;

@@ -34,9 +34,18 @@ __device__ __forceinline__ const T& ir_const_ref(const T* p, int i) {
 #endif
 }
 
+// Specialised build (MMB_IR_JIT, engine.cpp ir_jit_source -> hipRTC): the model's node log
+// densities and Logical expressions are generated as straight-line code before this header
+// (mmb_jit_block_lp, mmb_jit_logical: the interpreter's operations in the interpreter's order,
+// so results are bit-identical), and DMAX is the widest AMM block of the scheme (MMB_IR_DMAX),
+// so the unrolled factorization has no steps past it.  The LDS layout (TP, DP) is unchanged.
+#ifndef MMB_IR_DMAX
+#define MMB_IR_DMAX 32
+#endif
+
 template <>
 struct Mdl<MMB_MODEL_IR> {
-  static constexpr int G = 32, R = 1, DMAX = 32, DP = 32, TP = 528, VS = 0, PMON = 0;
+  static constexpr int G = 32, R = 1, DMAX = MMB_IR_DMAX, DP = 32, TP = 528, VS = 0, PMON = 0;
   // AMM scratch: mat[TP] | z2 | vv | mv | ia, then pchol32's reciprocal slot prow[DMAX]
   static constexpr int AMM_DBL = TP + 4 * DP + 2;
   static constexpr int LDS_DBL = 0;  // runtime layout: lds_stride()
@@ -198,6 +207,9 @@ struct Mdl<MMB_MODEL_IR> {
   __device__ static double logf(const SweepArgs& A, const DBlock& B, const St& s, const Lc&, const Grp<G>& g,
                                 const double* x) {
     put(B, s, g.lane, x, s.prop, nullptr);
+#ifdef MMB_IR_JIT
+    return mmb_jit_block_lp(A, B.ir_blk, s.prop, g, B.transform);
+#else
     const mmb_ir_block& IB = ir_const_ref(A.ir_blocks, B.ir_blk);
     double lp = 0.0;
     for (int t = 0; t < IB.nterms; ++t) {
@@ -205,6 +217,7 @@ struct Mdl<MMB_MODEL_IR> {
       if (!isfinite(lp)) break;
     }
     return lp;
+#endif
   }
   __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep&, const St& s,
                                                   const Lc& l, const Grp<G>& g, const double* x) {
@@ -240,9 +253,14 @@ struct Mdl<MMB_MODEL_IR> {
     grp_sync();
     int col = 0;
     for (int q = 0; q < A.ir_nmon; ++q) {
-      const mmb_ir_node& N = ir_const_ref(A.ir_nodes, ir_const_ref(A.ir_mon, q));
+      const int nid = ir_const_ref(A.ir_mon, q);
+      const mmb_ir_node& N = ir_const_ref(A.ir_nodes, nid);
       for (int i = g.lane; i < N.len; i += G) {
+#ifdef MMB_IR_JIT
+        const double v = N.family == MMB_IR_LOGICAL ? mmb_jit_logical(A, nid, i, s.cur)
+#else
         const double v = N.family == MMB_IR_LOGICAL ? ev(A, N.expr[0], i, s.cur, s.stk, g.lane)
+#endif
                                                     : (N.fixed ? A.ir_pool + N.off : s.cur + N.off)[i];
         A.draws[(size_t)(row * A.ir_pmon + col + i) * A.K + c] = v;
       }

@@ -24,8 +24,10 @@
 #ifndef MMB_MATH_H
 #define MMB_MATH_H
 
+#if !defined(__HIPCC_RTC__)
 #include <stdint.h>
 #include <math.h>
+#endif
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define MMB_HD __host__ __device__ static inline

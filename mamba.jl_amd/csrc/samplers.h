@@ -604,7 +604,7 @@ struct Smp {
           int p = 0;
           // one compare for the stop and the bookkeeping's ballot (pos = the complement mask)
           const uint64_t negm = __ballot(mx < 0);
-          bool pos = __builtin_amdgcn_inverse_ballot_w64(~negm);  // dpstf2's ajj <= 0 stop
+          bool pos = mmb_inverse_ballot(~negm);  // dpstf2's ajj <= 0 stop
           bool fast = true;
 #ifdef MMB_PCHOL_ONECOPY
           {
@@ -657,7 +657,7 @@ struct Smp {
             // out-of-range -inf lanes, which changes nothing that is used)
             // POSTHOC: no pivot on a stopping chain's step (its done lanes keep pe and row)
             const bool piv = CHECKED ? lane == p
-                                     : POSTHOC ? __builtin_amdgcn_inverse_ballot_w64(eq & ~negm) : key == mx;
+                                     : POSTHOC ? mmb_inverse_ballot(eq & ~negm) : key == mx;
             if (piv) {
               if constexpr (POSTHOC) apiv = dl;  // (pks: only the checked pass replays it)
               else pks[j] = p;
@@ -752,7 +752,7 @@ struct Smp {
             // pass checks, |lij| <= sqrt(Sigma_ll) < 2^350 for the PSD moment matrix, so work
             // stays finite; a -inf diagonal needs an overflowed Mv^2, whose Mvv is inf too: NaN.)
             const uint32_t tie = ((elo & (elo - 1)) & (nlo ? 0u : ~0u)) | ((ehi & (ehi - 1)) & (nhi ? 0u : ~0u));
-            needl = needl | __builtin_amdgcn_inverse_ballot_w64(bad | tiny | (tie ? ~0ull : 0ull));
+            needl = needl | mmb_inverse_ballot(bad | tiny | (tie ? ~0ull : 0ull));
           }
         }
       }
@@ -799,18 +799,18 @@ struct Smp {
 #else
     if constexpr (OPT) {
 #if defined(MMB_EXP_FORCEFAST) || defined(MMB_EXP_NOREDO)
-      (void)pass(std::false_type{});  // timing experiments only: the optimistic pass alone
+      (void)pass(mmb_bc<false>{});  // timing experiments only: the optimistic pass alone
 #elif defined(MMB_PCHOL_EXACT_NOINLINE)
-      if (pass(std::false_type{}))    // rare: redo with dpstf2's exact decisions, out of line
+      if (pass(mmb_bc<false>{}))    // rare: redo with dpstf2's exact decisions, out of line
         return pchol32_exact(d, mat, prow, pks, pos_out, NB, seed, xepoch, c, chain, it, b, m);
 #elif defined(MMB_PCHOL_COMPACT_REDO)
-      if (pass(std::false_type{})) {  // rare: redo with dpstf2's exact decisions, compact loop
+      if (pass(mmb_bc<false>{})) {  // rare: redo with dpstf2's exact decisions, compact loop
         redo_exact(d, mat, prow, pks, diag0, lc, inb, Lrow, work, done, pe);
       }
 #else
       // rare (a few per thousand factorizations): redo with dpstf2's exact decisions; marked
       // unlikely so the block placement moves the checked pass out of the hot code
-      if (__builtin_expect(pass(std::false_type{}), 0)) {
+      if (__builtin_expect(pass(mmb_bc<false>{}), 0)) {
         if (redo_out) *redo_out = 1;
         work = inb ? 0.0 : __builtin_inf();
 #pragma unroll
@@ -818,11 +818,11 @@ struct Smp {
         done = !inb;
         pe = 0;
         live = true;
-        (void)pass(std::true_type{});
+        (void)pass(mmb_bc<true>{});
       }
 #endif
     } else {
-      (void)pass(std::true_type{});
+      (void)pass(mmb_bc<true>{});
     }
 #endif
     {
@@ -1233,8 +1233,8 @@ struct Smp {
           }
         }
       };
-      if (fresh) slots(std::true_type{});
-      else slots(std::false_type{});
+      if (fresh) slots(mmb_bc<true>{});
+      else slots(mmb_bc<false>{});
 #pragma unroll
       for (int u = 0; u < NT; ++u)
         if ((u + 1) * G <= TP || u * G + g.lane < TP) Mvv_l[u * G] = lt[u];

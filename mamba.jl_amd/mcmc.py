@@ -157,6 +157,15 @@ class Engine:
             out[b] = {"updates": r[0], "full_rank": r[1], "rank_sum": r[2], "steps_sum": r[3], "redo": r[4]}
         return out
 
+    def ir_jit(self):
+        """Node-IR engines: (True, info) when the specialised kernel runs (mmb_create_ir compiled
+        the model with hipRTC or found it in the cache), (False, reason) for the interpreter."""
+        buf = C.create_string_buffer(4096)
+        r = self.lib.mmb_ir_jit_info(self.h, buf, len(buf))
+        if r < 0:
+            self._chk(r)
+        return bool(r), buf.value.decode()
+
     def state_bytes(self):
         b = C.c_double()
         self.lib.mmb_state_bytes(self.h, C.byref(b))

@@ -59,8 +59,11 @@ def example(mamba, name, K, seed=5, scheme=None):
     return m, m.init_matrix(inits, K)
 
 
-def run_both(mamba, oracle, m, V, iters, burnin, thin, seed=11):
+def run_both(mamba, oracle, m, V, iters, burnin, thin, seed=11, jit=True):
     eng = mamba.Engine(m)
+    # the specialised kernel (ir_jit.cpp, hipRTC; cached by tools/jit_prebuild.py) unless the
+    # interpreter was asked for with MMB_IR_JIT=0
+    assert eng.ir_jit()[0] == jit, eng.ir_jit()
     eng.init_chains(V, seed=seed)
     dg = eng.run(iters, burnin=burnin, thin=thin)
     st = oracle.new_state(m, V)
@@ -84,24 +87,37 @@ CASES = {
 }
 
 
+@pytest.mark.parametrize("kernel", ["specialised", "interpreter"])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_ir_gpu_vs_oracle(mamba, oracle, case):
+def test_ir_gpu_vs_oracle(mamba, oracle, case, kernel, monkeypatch):
+    """Both device forms of the node IR -- the model compiled to straight-line code at
+    mmb_create_ir (hipRTC) and the generic interpreter (MMB_IR_JIT=0) -- equal the oracle's
+    restatement bit for bit."""
+    if kernel == "interpreter":
+        monkeypatch.setenv("MMB_IR_JIT", "0")
     name, sch = CASES[case]
     m, V = example(mamba, name, 96, scheme=sch(mamba) if sch else None)
-    eng, dg, st, do = run_both(mamba, oracle, m, V, 60, 20, 2)
+    eng, dg, st, do = run_both(mamba, oracle, m, V, 60, 20, 2, jit=kernel == "specialised")
     np.testing.assert_array_equal(dg, do)
     np.testing.assert_array_equal(eng.values(), st["values"])
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
 
 
-def test_ir_rats_reference_scheme_gpu_vs_oracle(mamba, oracle):
+def test_ir_rats_reference_scheme_gpu_vs_oracle(mamba, oracle, monkeypatch):
+    """rats through the node IR with the reference Slice + AMWG scheme (rats.jl:112-116): the
+    specialised kernel, the interpreter and the oracle agree bit for bit."""
     scheme = mamba.model.rats_scheme_reference()
-    m = mamba.ir.rats_model().setinputs(mamba.ir.rats_inputs()).setsamplers(scheme)
     base = mamba.model.RATS_INITS
     inits = [{**base[k % 2], "y": mamba.model.RATS_Y} for k in range(64)]
+    m = mamba.ir.rats_model().setinputs(mamba.ir.rats_inputs()).setsamplers(scheme)
     V = m.init_matrix(inits, 64)
     eng, dg, st, do = run_both(mamba, oracle, m, V, 40, 10, 2)
     np.testing.assert_array_equal(dg, do)
+    monkeypatch.setenv("MMB_IR_JIT", "0")
+    m2 = mamba.ir.rats_model().setinputs(mamba.ir.rats_inputs()).setsamplers(scheme)
+    V2 = m2.init_matrix(inits, 64)
+    eng2, dg2, _, _ = run_both(mamba, oracle, m2, V2, 40, 10, 2, jit=False)
+    np.testing.assert_array_equal(dg2, dg)
 
 
 @pytest.mark.parametrize("name", ["seeds", "pumps", "surgical", "dyes", "salm", "blocker"])

@@ -245,3 +245,49 @@ def test_ir_create_validates_before_touching_the_device(mamba):
         m._ir_keep["code"][:] = keep
     sp.blocks[0].sampler = mamba.abi.MMB_SAMPLER_GIBBS
     assert lib.mmb_create_ir(C.byref(sp), C.byref(ir), 0, C.byref(h)) == -2
+
+
+def _jit_source(mamba, m):
+    import ctypes as C
+    lib = mamba.abi.lib()
+    spec, irm = m.spec(), m.ir()
+    n = lib.mmb_ir_jit_source_text(C.byref(spec), C.byref(irm), None, 0)
+    buf = C.create_string_buffer(n + 1)
+    lib.mmb_ir_jit_source_text(C.byref(spec), C.byref(irm), buf, n + 1)
+    return buf.value.decode()
+
+
+def test_ir_specialised_source_is_straight_line(mamba):
+    """mmb_create_ir's specialisation (csrc/ir_jit.cpp): the rats model with the reference scheme
+    as HIP source -- y's MvNormal over the 150 observations with its mean alpha[rat] + beta[rat] *
+    (x[j] - xbar) as four statements (two gathers, a data load, a multiply-add pair in the
+    interpreter's order), one function per node and one case per block, no code-word dispatch,
+    the sweep kernel instantiated for the scheme's sampler kinds only (Slice + AMWG)."""
+    ir = mamba.ir
+    m = ir.rats_model().setinputs(ir.rats_inputs()).setsamplers(mamba.model.rats_scheme_reference())
+    m.init_matrix([{**mamba.model.RATS_INITS[k % 2], "y": mamba.model.RATS_Y} for k in range(2)], 2)
+    src = _jit_source(mamba, m)
+    assert "ir_code" not in src and "mmb_jit_block_lp" in src
+    assert src.count("case ") >= len(m.samplers)
+    kinds = 0
+    for s in m.samplers:
+        kinds |= 1 << s.kind
+    assert f"sweep_body<MMB_MODEL_IR, {kinds}u>" in src
+    # the y node's mean: gather alpha, gather beta, the data column, t3 * t4, t2 + t5
+    assert "const double t5 = t3 * t4;" in src and "const double t6 = t2 + t5;" in src
+    assert "d_iso(150, sig, ss)" in src
+
+
+def test_ir_specialised_kernel_compiles_without_a_device(mamba):
+    """hipRTC compiles the specialised kernel on the CPU build host (mmb_ir_jit_prebuild: the
+    same validation as mmb_create_ir, then compile into the code-object cache)."""
+    import ctypes as C
+    ir = mamba.ir
+    m = ir.line_model().setinputs(mamba.model.LINE_DATA).setsamplers([mamba.AMWG(["beta", "s2"], 1.0)])
+    v = mamba.model.line_init_matrix(2, seed=1)
+    m.init_matrix([{"y": [1.0, 3, 3, 3, 5], "beta": v[k, :2], "s2": v[k, 2]} for k in range(2)], 2)
+    lib = mamba.abi.lib()
+    buf = C.create_string_buffer(8192)
+    rc = lib.mmb_ir_jit_prebuild(C.byref(m.spec()), C.byref(m.ir()), buf, len(buf))
+    assert rc == 0, buf.value.decode()
+    assert buf.value.decode().startswith(("cache hit", "compiled in"))
