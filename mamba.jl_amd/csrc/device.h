@@ -138,6 +138,7 @@ struct SweepArgs {
   int32_t ir_vs;         // doubles per chain row of `vals` (P rounded up to 32)
   int32_t ir_amm;        // AMM scratch doubles at the start of a chain's LDS (0 without AMM)
   int32_t ir_lds;        // LDS doubles per chain
+  const int32_t* cperm;  // lane-group slot -> chain (null: identity), engine.cpp order_chains
 };
 
 // Block descriptors are read-only for a launch: read them through the constant address

@@ -84,6 +84,8 @@ struct mmb_engine {
   hipEvent_t lg_cev[2] = {nullptr, nullptr};  // request-count readbacks in flight (run_logistic)
   int64_t lg_steps = 0;  // gradient steps of the last window
   unsigned long long* lg_ngrad = nullptr;
+  int32_t* d_cperm = nullptr;  // lane-group slot -> chain of the 32-lane sweep kernels (order_chains)
+  bool cperm_identity = true;
   unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum}, Slice overflows
                                           // since init_chains
   unsigned long long slice_overflows = 0;  // d_nstat[3] as last reported by mmb_run
@@ -672,6 +674,9 @@ static void free_dev(mmb_engine* e) {
     e->lg_ngrad = nullptr;
     if (e->d_nstat) (void)hipFree(e->d_nstat);
     e->d_nstat = nullptr;
+    if (e->d_cperm) (void)hipFree(e->d_cperm);
+    e->d_cperm = nullptr;
+    e->cperm_identity = true;
   }
   if (e->d_draws) (void)hipFree(e->d_draws);
   e->d_vals = nullptr;
@@ -1006,6 +1011,7 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.nuts_stat = e->d_nstat;
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
+  A.cperm = e->cperm_identity ? nullptr : e->d_cperm;
   if (e->model == MMB_MODEL_IR) {
     A.ir_nodes = e->d_ir_nodes; A.ir_code = e->d_ir_code; A.ir_const = e->d_ir_const;
     A.ir_pool = e->d_ir_pool; A.ir_blocks = e->d_ir_blocks; A.ir_mon = e->d_ir_mon;
@@ -1044,6 +1050,52 @@ static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
   HIPCHK(e, hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
   return 0;
 }
+
+// Wavefront pairing of the 32-lane kernels (two chains per wavefront step together): a chain whose
+// AMM moment matrix is indefinite stops its pivoted Cholesky after a few pivots every update
+// (the amm.jl:102 alias leaves about half the chains so, persistently), but its
+// wavefront runs until the partner chain has finished.  Before a window the engine orders the
+// chains by class -- for each AMM block, whether the chain has a valid factor (flags bit 2) --
+// so chains of one class share wavefronts; the kernel maps lane-group slot -> chain through
+// the table (sweep.h), and every chain keeps its own state, draws column and Philox id, so the
+// results are identical for any order.  MMB_ORDER_CHAINS=0 keeps the identity.
+static int order_chains(mmb_engine* e) {
+  if (!(e->model == MMB_MODEL_RATS || e->model == MMB_MODEL_IR) || e->K < 4) return 0;
+  std::vector<const BlockHost*> amm;
+  for (const BlockHost& h : e->blocks)
+    if (h.spec.sampler == MMB_SAMPLER_AMM && h.flags) amm.push_back(&h);
+  const char* env = std::getenv("MMB_ORDER_CHAINS");
+  const bool off = env && std::string(env) == "0";
+  if (amm.empty() || off) {
+    e->cperm_identity = true;
+    return 0;
+  }
+  const int64_t K = e->K;
+  std::vector<uint32_t> cls((size_t)K, 0u);
+  std::vector<int32_t> fl;
+  for (size_t a = 0; a < amm.size() && a < 16; ++a) {
+    int rc = d2h(e, fl, amm[a]->flags, (size_t)K);
+    if (rc) return rc;
+    for (int64_t k = 0; k < K; ++k) cls[k] |= (uint32_t)((fl[k] >> 2) & 1) << a;
+  }
+  std::vector<int32_t> perm((size_t)K);
+  std::vector<std::pair<uint32_t, int32_t>> key((size_t)K);
+  for (int64_t k = 0; k < K; ++k) key[k] = {cls[k], (int32_t)k};
+  std::stable_sort(key.begin(), key.end(),
+                   [](const std::pair<uint32_t, int32_t>& x, const std::pair<uint32_t, int32_t>& y) {
+                     return x.first < y.first;
+                   });
+  bool ident = true;
+  for (int64_t k = 0; k < K; ++k) {
+    perm[k] = key[k].second;
+    ident = ident && perm[k] == (int32_t)k;
+  }
+  e->cperm_identity = ident;
+  if (ident) return 0;
+  if (!e->d_cperm) HIPCHK(e, dalloc(&e->d_cperm, (size_t)K));
+  return h2d(e, e->d_cperm, perm);
+}
+
 
 // Config-4 window: ctl / grad kernel pairs until no chain requests a gradient.  The
 // request count is read back every LG_CHECK steps (pinned host words, one check behind the
@@ -1185,6 +1237,11 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
     }
   }
   if (e->model == MMB_MODEL_LOGISTIC) return run_logistic(e, a, (want && nk > 0) ? e->d_draws : nullptr, kept0, nk, want);
+  if (a->iters > 0) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // the flags of the previous window
+    int orc = order_chains(e);
+    if (orc) return orc;
+  }
   SweepArgs A;
   fill_args(e, A);
   A.burnin = a->burnin;

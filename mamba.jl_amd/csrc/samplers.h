@@ -94,10 +94,16 @@ struct Smp {
     if (adapt) m += 1;
     const typename M::Prep pc = M::prep(B, s);
     double logf0 = M::logf_p(A, B, pc, s, l, g, x);
+    // the proposal normals and (lane groups) the accept uniforms of every element at once,
+    // element e on its own lane: the same Philox draws (index e) the sequential loop below
+    // consumes, so the values are bit-identical; each step then takes its uniform from lane e
+    // (readlane) instead of every lane recomputing it (-~60 VALU per coordinate)
+    double uown[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       int e = r * G + g.lane;
       z[r] = e < d ? sig[r] * mmb_normal(&rn, 2u * (uint32_t)e) : 0.0;
+      uown[r] = (G > 1 && e < d) ? mmb_uniform(&ru, (uint32_t)e) : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -108,7 +114,8 @@ struct Smp {
         double xo = x[r];
         if (own) x[r] += z[r];
         double lpp = M::logf_p(A, B, pc, s, l, g, x);
-        if (mmb_uniform(&ru, (uint32_t)e) < mmb_exp(lpp - logf0)) {
+        const double ue = G == 32 ? lane_value(uown[r], ln) : mmb_uniform(&ru, (uint32_t)e);
+        if (ue < mmb_exp(lpp - logf0)) {
           logf0 = lpp;
           if (own) acc[r] += ad;
         } else if (own) {
@@ -1308,6 +1315,22 @@ struct Smp {
   __device__ __forceinline__ static double width(const DBlock& B, int e) {
     return B.width ? B.width[e] : B.width0;
   }
+  // The sequential uniforms of a lane group's update (Slice, univariate) 32 at a time: lane j of
+  // the group draws index base + j (the same Philox draws, bit-identical), a step takes its index
+  // from its lane (ds_bpermute: the two groups of a wave may be at different indices); a group
+  // that runs past the window refills it.  Replaces one all-lane Philox per draw.
+  struct UWin {
+    double u;
+    uint32_t base;
+  };
+  __device__ __forceinline__ static double uwin_next(const mmb_rng& ru, UWin& w, uint32_t k, const Grp<G>& g) {
+    if (k - w.base >= (uint32_t)G) {  // group-uniform
+      w.base = k;
+      w.u = mmb_uniform(&ru, k + (uint32_t)g.lane);
+    }
+    const int src = (int)(threadIdx.x & 63 & ~(G - 1)) + (int)(k - w.base);
+    return __shfl(w.u, src, 64);
+  }
   // slice.jl:66-92 (Univariate)
   __device__ __forceinline__ static void slice_uni(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
                                    const Lc& l, const Grp<G>& g) {
@@ -1325,15 +1348,20 @@ struct Smp {
       } else { lo[r] = 0.0; up[r] = 0.0; }
     }
     uint32_t k = (uint32_t)d;
+    UWin uw{0.0, 0xffffffffu - (uint32_t)G};  // empty window: the first draw fills it
+    auto next_u = [&](uint32_t kk) __attribute__((always_inline)) -> double {
+      if constexpr (G == 32) return uwin_next(ru, uw, kk, g);
+      else return mmb_uniform(&ru, kk);
+    };
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       for (int ln = 0; ln < G; ++ln) {
         int e = r * G + ln;
         if (e >= d) break;
         bool own = g.lane == ln;
-        double p0 = logf0 + mmb_log(mmb_uniform(&ru, k++));
+        double p0 = logf0 + mmb_log(next_u(k++));
         double xo = x[r];
-        double u = mmb_uniform(&ru, k++);
+        double u = next_u(k++);
         if (own) x[r] = lo[r] + (up[r] - lo[r]) * u;
         bool hit = false;
         for (int guard = 0; guard < MMB_SLICE_MAX_SHRINK; ++guard) {
@@ -1344,7 +1372,7 @@ struct Smp {
             if (value < xo) lo[r] = value;
             else up[r] = value;
           }
-          u = mmb_uniform(&ru, k++);
+          u = next_u(k++);
           if (own) x[r] = lo[r] + (up[r] - lo[r]) * u;
         }
         if (!hit) slice_overflow(A, g);

@@ -42,8 +42,13 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& A) {
     S::ik_fill();
     __syncthreads();
   }
-  const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
-  if (c >= A.K) return;  // whole lane groups exit together
+  const int slot = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
+  if (slot >= A.K) return;  // whole lane groups exit together
+  // chain of this lane group: the engine may order the chains so that chains whose pivoted
+  // Cholesky stops early share wavefronts (engine.cpp order_chains); every index below --
+  // state, tune, draws column, Philox chain id -- is the chain's own, so results do not depend
+  // on the order
+  const int c = A.cperm != nullptr ? A.cperm[slot] : slot;
   Grp<G> g;
   double* lds = smem + (size_t)(threadIdx.x / G) * M::lds_stride(A);
   typename M::St s;

@@ -134,6 +134,31 @@ def test_amm_stats_match_oracle(mamba, oracle, case, monkeypatch):
         assert 0.3 < sg[1]["full_rank"] / sg[1]["updates"] < 0.8
 
 
+def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
+    """engine.cpp order_chains pairs chains of one factor-validity class in a wavefront before
+    every window (the second window below runs permuted: the first set the flags).  Every chain
+    keeps its own state, draws column and Philox id, so the draws, values and tune equal the
+    identity-order run (MMB_ORDER_CHAINS=0) and the oracle bit for bit."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_ls(16384, seed=1000)[:600]
+    out = {}
+    for mode in ("ordered", "identity"):
+        if mode == "identity":
+            monkeypatch.setenv("MMB_ORDER_CHAINS", "0")
+        eng = mamba.Engine(m)
+        eng.init_chains(init, seed=33)
+        a = eng.run(90, burnin=0, thin=3)
+        b = eng.run(60, burnin=0, thin=3)
+        out[mode] = (a, b, eng.values(), eng.tune())
+    for x, y in zip(out["ordered"], out["identity"]):
+        np.testing.assert_array_equal(x, y)
+    st = oracle.new_state(m, init)
+    do = oracle.run(m, st, 150, burnin=0, thin=3, seed=33, nthreads=8)
+    np.testing.assert_array_equal(np.concatenate(out["ordered"][:2]), do)
+    tv = out["ordered"][3]
+    assert 0.2 < (tv[:, 2] != 0).mean() < 0.9  # alpha factor validity split: the order is not the identity
+
+
 def test_restart_and_sharding(mamba, oracle):
     m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
     init = mamba.model.rats_init_ls(128, seed=3)

@@ -8,12 +8,20 @@ between-chain SD of those means / sqrt(K).
   blocks frozen (adapt=:none): s2_c, mu_beta, alpha0 within 5 combined MCSE of the
   published means;
 * Gibbs + AMM with adapt=:all (the headline workload): mu_beta and alpha0 within 5 MCSE of
-  the published means; s2_c is biased LOW.  That is a property of the always-adapting
-  proposal of amm.jl:73-91, not of this engine: tests/golden/make_rats_amm_restatement.py,
-  an independent numpy restatement (numpy RNG, batched plain Cholesky of the same Sigma),
-  run on the same inits and schedule (rats_init_ls(16384, seed=1)[:4096], 10000 / 2500 / 2)
-  gives tests/golden/rats_amm_restatement.json; all three GPU means must lie within 5
-  combined standard errors of it."""
+  the published means; s2_c is biased LOW.  That is a property of the reference algorithm,
+  not of this engine: setadapt! aliases tune.Mv to the variate (amm.jl:102, `tune.Mv = v`), so
+  in every chain whose first adaptive proposal was accepted Mvv - Mv Mv' starts as
+  (v0 v0' - v1 v1') / 2, indefinite at the scale |v| |v1 - v0|, and the running averages shrink
+  it only like 2 / (m + 1); dpstf2 then stops after a few pivots every update and SigmaLm stays
+  at setadapt!'s zeros (amm.jl:88-90, 104), so about half the alpha chains (a third of the beta
+  chains) propose 0.05 SigmaL z1 only -- steps far below the posterior sd -- and hug their
+  per-rat fits, which biases s2_c low (the mechanism is pinned on the oracle by
+  tests/test_oracle.py::test_rats_amm_alias_leaves_first_accepted_chains_without_factor).
+  tests/golden/make_rats_amm_restatement.py, an independent numpy restatement (numpy RNG,
+  batched plain Cholesky of the same Sigma, the same alias), run on the same inits and
+  schedule (rats_init_ls(16384, seed=1)[:4096], 10000 / 2500 / 2) gives
+  tests/golden/rats_amm_restatement.json; all three GPU means must lie within 5 combined
+  standard errors of it."""
 import json
 import os
 
