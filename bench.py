@@ -411,8 +411,13 @@ def main():
         kms, launches = t_kms, t_launches
         flops = 4.0 * 10000 * 50 * grads_timed
         achieved = flops / (kms * 1e-3) / 1e12
+        # the same flops over the window's wall time: the gradient launches are 77 % of it, the
+        # control kernel (NUTS machines, partial folding) 22 %, launch gaps 0.5 % (rocprofv3 trace,
+        # profiles/r4_logistic_walltime_split.json)
+        wall_tfs = flops / dt / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None,
+                "achieved_wall": wall_tfs, "frac_wall": wall_tfs / F64_MFMA_PEAK_TFS,
                 "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": 4.0 * 10000 * 50,
                 "avg_launch_ms": kms / launches, "gradients_per_launch": grads_timed / launches,
                 "gradients_per_chain_update_timed": grads_timed / (K * args.steps),
@@ -420,9 +425,10 @@ def main():
     else:
         W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
                                "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "256"))
-        nroof = max(W * 16, 64)
-        eng.run(nroof, burnin=0, thin=thin, model_burnin=0, draws=False, keep_device=False, time_kernels=True)
-        kms, launches, units = eng.kernel_time()
+        # the timed window's own launches, HIP events on the engine stream (measured before the
+        # collective: a separate window after it started on a GPU clocked down during the RCCL
+        # init's idle seconds and read ~10 % slow)
+        kms, launches, units = t_kms, t_launches, t_units
         per_update = eng.state_bytes() + 8.0 * eng.pmon / thin  # 2*S_state + S_draw/thin
         bytes_per_launch = per_update * units / launches
         avg_ms = kms / launches

@@ -1056,7 +1056,7 @@ static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
 // (the amm.jl:102 alias leaves about half the chains so, persistently), but its
 // wavefront runs until the partner chain has finished.  Before a window the engine orders the
 // chains by class -- for each AMM block, whether the chain has a valid factor (flags bit 2) --
-// so chains of one class share wavefronts; the kernel maps lane-group slot -> chain through
+// so chains that stop alike share wavefronts; the kernel maps lane-group slot -> chain through
 // the table (sweep.h), and every chain keeps its own state, draws column and Philox id, so the
 // results are identical for any order.  MMB_ORDER_CHAINS=0 keeps the identity.
 static int order_chains(mmb_engine* e) {
@@ -1071,12 +1071,16 @@ static int order_chains(mmb_engine* e) {
     return 0;
   }
   const int64_t K = e->K;
+  // key: per AMM block (first block most significant), whether the chain has a valid factor;
+  // the sort is stable, so chains of a class stay in index order (neighbouring slots keep
+  // neighbouring state rows: adding the mean rank to the key, which scatters them, measured 8 %
+  // slower although it pairs the stopping steps more closely)
   std::vector<uint32_t> cls((size_t)K, 0u);
   std::vector<int32_t> fl;
   for (size_t a = 0; a < amm.size() && a < 16; ++a) {
     int rc = d2h(e, fl, amm[a]->flags, (size_t)K);
     if (rc) return rc;
-    for (int64_t k = 0; k < K; ++k) cls[k] |= (uint32_t)((fl[k] >> 2) & 1) << a;
+    for (int64_t k = 0; k < K; ++k) cls[k] = (cls[k] << 1) | (uint32_t)((fl[k] >> 2) & 1);
   }
   std::vector<int32_t> perm((size_t)K);
   std::vector<std::pair<uint32_t, int32_t>> key((size_t)K);

@@ -988,12 +988,14 @@ struct Smp {
       ws = max((uint32_t)act != 0u ? s0 : 0, (act >> 32) != 0u ? s1 : 0);
     }
     if (g.lane == 0) {
+      // no-return atomics: fire-and-forget, no HBM round trip on the update's path (a plain
+      // load-add-store would wait for the load)
       uint32_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
-      a[0] += 1u;
-      a[1] += rank == d ? 1u : 0u;
-      a[2] += (uint32_t)rank;
-      a[3] += (uint32_t)ws;
-      a[4] += (uint32_t)redo;
+      (void)__hip_atomic_fetch_add(a + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (rank == d) (void)__hip_atomic_fetch_add(a + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      (void)__hip_atomic_fetch_add(a + 2, (uint32_t)rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      (void)__hip_atomic_fetch_add(a + 3, (uint32_t)ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (redo) (void)__hip_atomic_fetch_add(a + 4, (uint32_t)redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
