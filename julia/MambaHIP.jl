@@ -102,6 +102,19 @@ function comm_init(engines::Vector{Ptr{Void}}, nranks::Integer=length(engines), 
   c[]
 end
 comm_destroy(c) = ccall((:mmb_comm_destroy, libmambahip), Void, (Ptr{Void},), c)
+# diagnostics: AMM factorization counters per sampling block (adaptive updates, rank(F) == n,
+# rank sum, executed steps, redone passes; amm.jl:81-90) and which node-IR kernel an engine runs
+const MMB_AMM_STATS = 5
+function amm_stats(e)
+  out = zeros(Int64, MMB_AMM_STATS, 8)
+  check(ccall((:mmb_amm_stats, libmambahip), Cint, (Ptr{Void}, Ptr{Int64}), e, out), e); out
+end
+function ir_jit_info(e)
+  buf = zeros(UInt8, 4096)
+  r = ccall((:mmb_ir_jit_info, libmambahip), Cint, (Ptr{Void}, Ptr{UInt8}, Int64), e, buf, length(buf))
+  r < 0 && check(r, e)
+  (r == 1, unsafe_string(pointer(buf)))
+end
 function range_allreduce(c, e, p::Integer)
   mm = Array{Float64}(2, p)
   check(ccall((:mmb_range_allreduce, libmambahip), Cint, (Ptr{Void}, Ptr{Float64}), c, mm), e); mm

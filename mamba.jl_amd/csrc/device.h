@@ -295,6 +295,19 @@ struct Grp {
       y += b;
     }
   }
+  // four independent sums, stage by stage (each as sum() would form it)
+  __device__ __forceinline__ void sum4(double& x, double& y, double& z, double& w) const {
+    if (G == 32) {
+      x += other_d<0>(x); y += other_d<0>(y); z += other_d<0>(z); w += other_d<0>(w);
+      x += other_d<1>(x); y += other_d<1>(y); z += other_d<1>(z); w += other_d<1>(w);
+      x += other_d<2>(x); y += other_d<2>(y); z += other_d<2>(z); w += other_d<2>(w);
+      x += other_d<3>(x); y += other_d<3>(y); z += other_d<3>(z); w += other_d<3>(w);
+      x += other_d<4>(x); y += other_d<4>(y); z += other_d<4>(z); w += other_d<4>(w);
+      return;
+    }
+    sum2(x, y);
+    sum2(z, w);
+  }
   __device__ __forceinline__ double bcast(double x, int src) const {
     if (G == 1) return x;
     int base = (int)(threadIdx.x & 63) & ~(G - 1);

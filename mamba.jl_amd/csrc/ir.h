@@ -223,6 +223,12 @@ struct Mdl<MMB_MODEL_IR> {
                                                   const Lc& l, const Grp<G>& g, const double* x) {
     return logf(A, B, s, l, g, x);
   }
+  __device__ __forceinline__ static void logf_p2(const SweepArgs& A, const DBlock& B, const Prep& c, const St& s,
+                                                 const Lc& l, const Grp<G>& g, const double* x, const double* v,
+                                                 double& lx, double& lv) {
+    lx = logf_p(A, B, c, s, l, g, x);
+    lv = logf_p(A, B, c, s, l, g, v);
+  }
   // logpdfgrad!(block, x, :forward) (sampler.jl:106-111): Calculus forward differences,
   // epsilon = sqrt(eps()) * max(1, |x_i|); non-finite gradient entries -> 0
   __device__ static double logf_grad(const SweepArgs& A, const DBlock& B, const St& s, const double* x,

@@ -187,6 +187,22 @@ struct Mdl<MMB_MODEL_RATS> {
     if (!isfinite(lp)) return lp;
     return lp + (-0.5 * (c.yk + ss * c.invv));
   }
+  // logpdf! at two block vectors (AMM: the proposal and the current value) with one joint
+  // butterfly of the four lane partials: each sum takes the same partners in the same order as
+  // logf_vec's, so both values are bit-identical to two logf_vec calls, with half the DPP
+  // dependency stages
+  __device__ __forceinline__ static void logf_vec2(const SweepArgs& A, const VecCtx& c, const St& s, const Lc& l,
+                                                   const Grp<G>& g, const double* x, const double* v, double& lx,
+                                                   double& lv) {
+    double px = normsum_lane(c.mu, c.sig, c.logsig, x, g.lane);
+    double sx = c.al ? ssr_lane(A, l, x, s.b, g.lane) : ssr_lane(A, l, s.a, x, g.lane);
+    double pv = normsum_lane(c.mu, c.sig, c.logsig, v, g.lane);
+    double sv = c.al ? ssr_lane(A, l, v, s.b, g.lane) : ssr_lane(A, l, s.a, v, g.lane);
+    g.sum4(px, sx, pv, sv);
+    const double ax = 0.0 + px, av = 0.0 + pv;
+    lx = isfinite(ax) ? ax + (-0.5 * (c.yk + sx * c.invv)) : ax;
+    lv = isfinite(av) ? av + (-0.5 * (c.yk + sv * c.invv)) : av;
+  }
   // block-update-invariant context (vector blocks); scalar blocks fall back to logf
   using Prep = VecCtx;
   __device__ __forceinline__ static Prep prep(const DBlock& B, const St& s) { return vec_ctx(B, s); }
@@ -195,6 +211,18 @@ struct Mdl<MMB_MODEL_RATS> {
                                                   const double* x) {
     if (is_vec(B.nodes[0])) return logf_vec(A, c, s, l, g, x);
     return logf(A, B, s, l, g, x);
+  }
+  __device__ __forceinline__ static void logf_p2(const SweepArgs& A, const DBlock& B, const Prep& c, const St& s,
+                                                 const Lc& l, const Grp<G>& g, const double* x, const double* v,
+                                                 double& lx, double& lv) {
+#ifndef MMB_EXP_LOGF1
+    if (is_vec(B.nodes[0])) {
+      logf_vec2(A, c, s, l, g, x, v, lx, lv);
+      return;
+    }
+#endif
+    lx = logf_p(A, B, c, s, l, g, x);
+    lv = logf_p(A, B, c, s, l, g, v);
   }
   // logpdf!(block, x)
   __device__ __forceinline__ static double logf(const SweepArgs& A, const DBlock& B, const St& s0, const Lc& l,
@@ -348,6 +376,12 @@ struct Mdl<MMB_MODEL_LINE> {
                                                   const St& s, const Lc& l, const Grp<G>& g,
                                                   const double* x) {
     return logf(A, B, s, l, g, x);
+  }
+  __device__ __forceinline__ static void logf_p2(const SweepArgs& A, const DBlock& B, const Prep& c, const St& s,
+                                                 const Lc& l, const Grp<G>& g, const double* x, const double* v,
+                                                 double& lx, double& lv) {
+    lx = logf_p(A, B, c, s, l, g, x);
+    lv = logf_p(A, B, c, s, l, g, v);
   }
   __device__ __forceinline__ static double ylp(const SweepArgs& A, const St& s) {
     double ssq = 0.0;

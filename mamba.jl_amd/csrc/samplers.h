@@ -586,6 +586,15 @@ struct Smp {
 #else
       constexpr bool POSTHOC = !CHECKED;
 #endif
+      // DW: the optimistic pass keeps no done flag: a lane is done iff its work is +inf (pivots set
+      // it; an undone lane whose sum of squares overflowed counts as done too, which only a chain
+      // that cannot reach full rank can meet -- its rank then disagrees with its steps and the
+      // post-hoc check redoes it)
+#ifdef MMB_PCHOL_DONEFLAG
+      constexpr bool DW = false;
+#else
+      constexpr bool DW = POSTHOC;
+#endif
       uint64_t needm = 0;  // wave-uniform: nonzero if a step of this pass was not decided exactly
       bool needl = false;  // per-lane form of needm (a lane mask: the OR stays on the scalar unit)
       double apiv = 1.0;   // POSTHOC: this lane's candidate when it was taken as the pivot
@@ -690,7 +699,7 @@ struct Smp {
               Lrow[j] = ajj;
               pe = j;
               work = inf_s;
-              done = true;
+              if constexpr (!DW) done = true;
             }
             grp_sync();
             if (j + 1 < d) {  // (j = d - 1: every lane is done)
@@ -733,9 +742,10 @@ struct Smp {
 #endif
               }
               const double lij = (sig - (t0 + t1)) * rinv;
+              const bool keep = DW ? work == inf_s : done;  // done lanes keep their rows
               // done lanes carry work = +inf, which absorbs lij^2: no select for work
               work = work + lij * lij;
-              if (!done) Lrow[j] = lij;
+              if (!keep) Lrow[j] = lij;
             }
             grp_sync();
             if (NOBR) live = live && pos;
@@ -773,6 +783,7 @@ struct Smp {
         //   the chain has more done lanes than steps that took pivots (pe values 0..max_pe, each
         //   taken once when exact: done == max_pe + 1).
         // On a tie the rows the pass computed after it are garbage; the redo replaces them.
+        if constexpr (DW) done = work == inf_s;
         const bool inr = apiv >= 0x1p-700 && apiv <= 0x1p700;
         uint64_t need = __ballot(inb && (done ? !inr : isnan(diag0 - work)));
         const uint64_t dn = __ballot(done && inb);
@@ -1152,8 +1163,8 @@ struct Smp {
     for (int r = 0; r < R; ++r) x[r] = x[r] + v[r];
     MMB_PROF_MARK(2, g.lane)
     const typename M::Prep pc = M::prep(B, s);
-    double lx = M::logf_p(A, B, pc, s, l, g, x);
-    double lv = M::logf_p(A, B, pc, s, l, g, v);
+    double lx, lv;
+    M::logf_p2(A, B, pc, s, l, g, x, v, lx, lv);
     const double ua = G == 32 ? upre : mmb_uniform(&ru, 0u);  // predraw() for 32-lane groups
     if (ua < mmb_exp(lx - lv)) {
 #pragma unroll

@@ -91,7 +91,7 @@ def census(ins):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r3_pchol32_isa_census.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_pchol32_isa_census.json"))
     a = ap.parse_args()
     ins = kernel_instructions(disassemble())
     steps = factorization_steps(ins)
