@@ -424,7 +424,7 @@ def main():
                 "window": f"timed run: {args.steps} iterations, burnin {tburn}"}
     else:
         W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
-                               "8" if args.workload == "rats" else "16" if args.workload.endswith("_ir") else "256"))
+                               "16" if args.workload == "rats" or args.workload.endswith("_ir") else "256"))
         # the timed window's own launches, HIP events on the engine stream (measured before the
         # collective: a separate window after it started on a GPU clocked down during the RCCL
         # init's idle seconds and read ~10 % slow)
@@ -485,7 +485,7 @@ def main():
     if args.workload != "rats":
         out["metric"] = f"chain-updates/sec on {args.workload} (not the headline metric)"
     if args.workload == "rats":
-        out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "8")),
+        out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "16")),
                               "scheme": args.scheme})
         if args.scheme == "gibbs_amm":
             out["config"]["amm_adapt"] = "all"

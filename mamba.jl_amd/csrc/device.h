@@ -199,6 +199,7 @@ __device__ __forceinline__ void fmac_rowbc(double& acc, double x, double b) {
     asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
                  : "+v"(acc) : "v"(x), "v"(b), "n"(N));
 }
+__device__ __forceinline__ void fmac_rowbc_nf(double& acc, double x, double b, int n, bool first);
 // n = k % 16 of a dot product over k ascending: the uses at k = 0 and k = 16 are first uses
 __device__ __forceinline__ void fmac_rowbc_n(double& acc, double x, double b, int n) {
   switch (n) {  // n is a constant after unrolling: one case survives
@@ -207,6 +208,17 @@ __device__ __forceinline__ void fmac_rowbc_n(double& acc, double x, double b, in
     MMB_RBC(8) MMB_RBC(9) MMB_RBC(10) MMB_RBC(11) MMB_RBC(12) MMB_RBC(13) MMB_RBC(14) MMB_RBC(15)
 #undef MMB_RBC
   }
+}
+
+// as fmac_rowbc_n for a source last written by an LDS read, not by a VALU instruction: the DPP
+// read-after-VALU-write hazard does not apply and no use needs wait states (tests/test_isa.py
+// checks the built code for VALU writes of every DPP source)
+__device__ __forceinline__ void fmac_rowbc_ld(double& acc, double x, double b, int n) {
+#ifdef MMB_EXP_DPPNOP
+  fmac_rowbc_n(acc, x, b, n);
+#else
+  fmac_rowbc_nf(acc, x, b, n, false);
+#endif
 }
 
 // as fmac_rowbc_n with the first use of the source at an explicit step (a dot product whose

@@ -736,8 +736,8 @@ struct Smp {
 #pragma unroll
                 for (int k = 0; k < j; ++k) {
                   const double src = k < 16 ? pA : pB;
-                  if (k & 1) fmac_rowbc_n(t1, src, Lrow[k], k & 15);
-                  else fmac_rowbc_n(t0, src, Lrow[k], k & 15);
+                  if (k & 1) fmac_rowbc_ld(t1, src, Lrow[k], k & 15);
+                  else fmac_rowbc_ld(t0, src, Lrow[k], k & 15);
                 }
 #endif
               }
@@ -931,8 +931,8 @@ struct Smp {
 #pragma unroll
             for (int k = 0; k < j; ++k) {
               const double src = k < 16 ? pA : pB;
-              if (k & 1) fmac_rowbc_n(t1, src, Lrow[k], k & 15);
-              else fmac_rowbc_n(t0, src, Lrow[k], k & 15);
+              if (k & 1) fmac_rowbc_ld(t1, src, Lrow[k], k & 15);
+              else fmac_rowbc_ld(t0, src, Lrow[k], k & 15);
             }
           }
 #endif
