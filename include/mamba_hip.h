@@ -42,7 +42,7 @@ typedef __UINTPTR_TYPE__ uintptr_t;
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 7
+#define MMB_ABI_VERSION 8
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -363,6 +363,13 @@ int mmb_ir_jit_source_text(const mmb_model_spec* spec, const mmb_ir_model* ir, c
  * window); no draw depends on them. */
 #define MMB_AMM_STATS 5
 int mmb_amm_stats(mmb_engine* e, int64_t* out /* MMB_MAX_BLOCKS x MMB_AMM_STATS */);
+
+/* AMWG path counter since init_chains: out[0] = block updates that ran amwg_sub! one coordinate
+ * at a time (samplers.h amwg) instead of the lane-parallel decision of every coordinate, which
+ * is taken when each coordinate's accept test is certain under the logpdf's rounding bound
+ * (rats alpha / beta; the environment variable MMB_AMWG_EXACT=1 forces the sequential loop).
+ * Both paths give the same draws; diagnostics only. */
+int mmb_amwg_stats(mmb_engine* e, int64_t* out /* 1 */);
 
 #ifdef __cplusplus
 }

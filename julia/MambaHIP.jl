@@ -109,6 +109,11 @@ function amm_stats(e)
   out = zeros(Int64, MMB_AMM_STATS, 8)
   check(ccall((:mmb_amm_stats, libmambahip), Cint, (Ptr{Void}, Ptr{Int64}), e, out), e); out
 end
+# AMWG block updates that ran the sequential coordinate loop (amwg_sub!, amwg.jl:97-115)
+function amwg_stats(e)
+  out = zeros(Int64, 1)
+  check(ccall((:mmb_amwg_stats, libmambahip), Cint, (Ptr{Void}, Ptr{Int64}), e, out), e); out[1]
+end
 function ir_jit_info(e)
   buf = zeros(UInt8, 4096)
   r = ccall((:mmb_ir_jit_info, libmambahip), Cint, (Ptr{Void}, Ptr{UInt8}, Int64), e, buf, length(buf))

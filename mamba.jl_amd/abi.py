@@ -14,7 +14,7 @@ MMB_MAX_NODES_PER_BLOCK = 4
 MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC, MMB_MODEL_IR = 1, 2, 3, 4
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
-MMB_ABI_VERSION = 7
+MMB_ABI_VERSION = 8
 MMB_GRAD_DEFAULT, MMB_GRAD_FORWARD, MMB_GRAD_ANALYTIC = 0, 1, 2
 MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
@@ -115,6 +115,7 @@ def _declare(lib):
         "mmb_grad_evals": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_nuts_stats": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_amm_stats": (C.c_int, [P, C.POINTER(I64)]),
+        "mmb_amwg_stats": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_ir_jit_info": (C.c_int, [P, C.c_char_p, I64]),
         "mmb_ir_jit_prebuild": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_char_p, I64]),
         "mmb_ir_jit_source_text": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_char_p, I64]),

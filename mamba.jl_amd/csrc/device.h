@@ -119,7 +119,8 @@ struct SweepArgs {
   double* vals;          // model-specific device layout
   int64_t xepoch;        // bumped by every host write of chain state (invalidates carried proposals)
   unsigned long long* nuts_stat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat),
-                                  // [3] Slice updates stopped at MMB_SLICE_MAX_SHRINK
+                                  // [3] Slice updates stopped at MMB_SLICE_MAX_SHRINK,
+                                  // [5] AMWG block updates that took the sequential path
   double* draws;         // [n_kept][pmon][K] or null
   const double* data0;   // model data (rats: y[150]; line: x[5], y[5] packed as 10)
   double ig_c;           // 0.001 log(0.001) - lgamma(0.001)
@@ -139,6 +140,8 @@ struct SweepArgs {
   int32_t ir_amm;        // AMM scratch doubles at the start of a chain's LDS (0 without AMM)
   int32_t ir_lds;        // LDS doubles per chain
   const int32_t* cperm;  // lane-group slot -> chain (null: identity), engine.cpp order_chains
+  int32_t amwg_exact;    // MMB_AMWG_EXACT: 1 = AMWG always takes the sequential path (samplers.h
+                         // amwg), 2 = certainty band widened 2^30 times (tests: frequent fallback)
 };
 
 // Block descriptors are read-only for a launch: read them through the constant address

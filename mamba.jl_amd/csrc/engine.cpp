@@ -1012,6 +1012,11 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
   A.cperm = e->cperm_identity ? nullptr : e->d_cperm;
+  {  // MMB_AMWG_EXACT=1: every AMWG update by the sequential loop; 2: wide certainty band
+    const char* ae = std::getenv("MMB_AMWG_EXACT");
+    const int v = ae ? std::atoi(ae) : 0;
+    A.amwg_exact = (v == 1 || v == 2) ? v : 0;
+  }
   if (e->model == MMB_MODEL_IR) {
     A.ir_nodes = e->d_ir_nodes; A.ir_code = e->d_ir_code; A.ir_const = e->d_ir_const;
     A.ir_pool = e->d_ir_pool; A.ir_blocks = e->d_ir_blocks; A.ir_mon = e->d_ir_mon;
@@ -1685,6 +1690,18 @@ int mmb_nuts_stats(mmb_engine* e, int64_t* out) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   for (int i = 0; i < 3; ++i) out[i] = (int64_t)v[i];
+  return 0;
+}
+
+int mmb_amwg_stats(mmb_engine* e, int64_t* out) {
+  if (!e || !out) return fail(e, MMB_E_ARG, "null argument");
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (e->d_nstat) {
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpyAsync(v, e->d_nstat, sizeof v, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  out[0] = (int64_t)v[5];
   return 0;
 }
 

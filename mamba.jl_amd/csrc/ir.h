@@ -201,6 +201,7 @@ struct Mdl<MMB_MODEL_IR> {
     put(B, s, g.lane, x, s.cur, s.prop);
   }
 
+  static constexpr bool AMWG_SEP = false;  // samplers.h amwg: sequential path only
   struct Prep {};
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   // logpdf!(m, x, block, transform)

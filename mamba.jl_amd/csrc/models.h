@@ -203,6 +203,23 @@ struct Mdl<MMB_MODEL_RATS> {
     lx = isfinite(ax) ? ax + (-0.5 * (c.yk + sx * c.invv)) : ax;
     lv = isfinite(av) ? av + (-0.5 * (c.yk + sv * c.invv)) : av;
   }
+  // AMWG on a vector block (samplers.h amwg, lane-parallel path): changing element j of alpha
+  // (beta) changes only lane j's prior term and lane j's part of the residual sum of squares, so
+  // logf_vec at any state is the same butterfly over per-lane terms, and the lane's two terms
+  // at its own element value are what logf_vec would form on that lane
+  static constexpr bool AMWG_SEP = true;
+  __device__ __forceinline__ static bool amwg_sep(const DBlock& B) { return is_vec(B.nodes[0]); }
+  __device__ __forceinline__ static void amwg_terms(const SweepArgs& A, const VecCtx& c, const St& s, const Lc& l,
+                                                    int lane, double xv, double& tp, double& ts) {
+    double xa[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) xa[r] = xv;
+    tp = normsum_lane(c.mu, c.sig, c.logsig, xa, lane);
+    ts = c.al ? ssr_lane(A, l, xa, s.b, lane) : ssr_lane(A, l, s.a, xa, lane);
+  }
+  // logf_vec = (0 + sum tp) + (-0.5 * (yk + (sum ts) * invv))
+  __device__ __forceinline__ static double amwg_yk(const VecCtx& c) { return c.yk; }
+  __device__ __forceinline__ static double amwg_invv(const VecCtx& c) { return c.invv; }
   // block-update-invariant context (vector blocks); scalar blocks fall back to logf
   using Prep = VecCtx;
   __device__ __forceinline__ static Prep prep(const DBlock& B, const St& s) { return vec_ctx(B, s); }
@@ -370,6 +387,7 @@ struct Mdl<MMB_MODEL_LINE> {
       }
     }
   }
+  static constexpr bool AMWG_SEP = false;  // samplers.h amwg: sequential path only
   struct Prep {};
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep&,

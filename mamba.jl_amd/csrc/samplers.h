@@ -70,6 +70,54 @@ struct Smp {
   }
 
   // ---------------------------------------------------------------- AMWG
+  // amwg_sub! decided for every coordinate at once (blocks whose logpdf is a butterfly over
+  // per-lane terms that only the lane's own element changes: M::AMWG_SEP).  Coordinate j's
+  // step compares its uniform with exp(delta_j), delta_j = logf(state with x_j') - logf0, two
+  // rounded evaluations whose states differ only in lane j's terms; in exact arithmetic the
+  // difference is d_j = (tp_j' - tp_j) - 0.5 invv (ts_j' - ts_j) whatever the other
+  // coordinates' accept history.  Each rounded logf is within 9 u (sum_i |tp_i| + |yk| +
+  // invv sum_i |ts_i|) of its exact value (a depth-5 tree sum, then three roundings), so
+  // |delta_j - d_j| <= eps_j with the factor of 128 u taken below; a decision is CERTAIN
+  // when the uniform is outside [exp(d_j - eps_j), exp(d_j + eps_j)] widened by the
+  // (sub-ulp) error of mmb_exp.  All certain: x_j' where accepted -- the same values and
+  // accept counts as the sequential loop, bit for bit, since certain decisions are its
+  // decisions.  Any uncertain lane, a non-finite term or bound: false, and the caller runs
+  // the sequential loop (RNG draws are the same precomputed z / uown either way).
+  __device__ __forceinline__ static bool amwg_lanes(const DBlock& B, const typename M::Prep& pc, const St& s,
+                                                    const Lc& l, const Grp<G>& g, double* x, const double* z,
+                                                    const double* uown, double* acc, double ad,
+                                                    const SweepArgs& A) {
+    const bool in = g.lane < B.d;
+    const double x1 = x[0] + z[0];  // the sequential loop's x[r] += z[r]
+    double tp0, ts0, tp1, ts1;
+    M::amwg_terms(A, pc, s, l, g.lane, x[0], tp0, ts0);
+    M::amwg_terms(A, pc, s, l, g.lane, x1, tp1, ts1);
+    const double invv = M::amwg_invv(pc), yk = M::amwg_yk(pc);
+    bool bad = !(isfinite(tp0) && isfinite(ts0) && isfinite(tp1) && isfinite(ts1));
+    double ap = fmax(fabs(tp0), fabs(tp1)), as = fmax(fabs(ts0), fabs(ts1));
+    g.sum2(ap, as);  // bounds of sum |terms| over both states
+    const double dp = tp1 - tp0, ds = ts1 - ts0;
+    const double del = dp + (-0.5 * invv) * ds;
+    const double mag = ap + fabs(yk) + invv * as;
+    // (amwg_exact = 2, tests: a 2^30 times wider band, so that many updates fall back)
+    const double eps = (A.amwg_exact == 2 ? 0x1p-16 : 0x1p-46) * (mag + fabs(dp) + invv * fabs(ds) + fabs(del));
+    const double lo = del - eps, hi = del + eps;
+    const double ue = uown[0];  // in [0, 1)
+    const bool acc_c = lo >= 700.0 || (lo > -700.0 && ue < mmb_exp(lo) * (1.0 - 0x1p-48));
+    const bool rej_c = (hi <= -700.0 && ue >= 1e-300) ||
+                       (hi > -700.0 && hi < 700.0 && ue >= mmb_exp(hi) * (1.0 + 0x1p-48));
+    bad = bad || !isfinite(eps) || !isfinite(invv) || !isfinite(yk);
+    const bool unsure = in && (bad || !(acc_c || rej_c));
+    const uint64_t bal = __ballot(unsure);
+    const bool any = (threadIdx.x & 32) ? (bal >> 32) != 0 : (uint32_t)bal != 0;
+    if (any) return false;
+    if (in && acc_c) {
+      x[0] = x1;
+      acc[0] += ad;
+    }
+    return true;
+  }
+
   // amwg.jl:68-115 (sample!, setadapt!, amwg_sub!).
   __device__ __forceinline__ static void amwg(const SweepArgs& A, const DBlock& B, int c, const mmb_rng& rn,
                               const mmb_rng& ru, bool adapt, St& s, const Lc& l, const Grp<G>& g) {
@@ -93,7 +141,6 @@ struct Smp {
     const double ad = adapt ? 1.0 : 0.0;
     if (adapt) m += 1;
     const typename M::Prep pc = M::prep(B, s);
-    double logf0 = M::logf_p(A, B, pc, s, l, g, x);
     // the proposal normals and (lane groups) the accept uniforms of every element at once,
     // element e on its own lane: the same Philox draws (index e) the sequential loop below
     // consumes, so the values are bit-identical; each step then takes its uniform from lane e
@@ -105,21 +152,31 @@ struct Smp {
       z[r] = e < d ? sig[r] * mmb_normal(&rn, 2u * (uint32_t)e) : 0.0;
       uown[r] = (G > 1 && e < d) ? mmb_uniform(&ru, (uint32_t)e) : 0.0;
     }
+    bool seq = true;
+    if constexpr (M::AMWG_SEP && G == 32 && R == 1) {
+      if (A.amwg_exact != 1 && M::amwg_sep(B)) {
+        seq = !amwg_lanes(B, pc, s, l, g, x, z, uown, acc, ad, A);
+        if (seq && g.lane == 0) atomicAdd(&A.nuts_stat[5], 1ull);
+      }
+    }
+    if (seq) {  // amwg_sub!: one coordinate at a time, the block's logpdf at every proposal
+      double logf0 = M::logf_p(A, B, pc, s, l, g, x);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      for (int ln = 0; ln < G; ++ln) {
-        int e = r * G + ln;
-        if (e >= d) break;
-        bool own = g.lane == ln;
-        double xo = x[r];
-        if (own) x[r] += z[r];
-        double lpp = M::logf_p(A, B, pc, s, l, g, x);
-        const double ue = G == 32 ? lane_value(uown[r], ln) : mmb_uniform(&ru, (uint32_t)e);
-        if (ue < mmb_exp(lpp - logf0)) {
-          logf0 = lpp;
-          if (own) acc[r] += ad;
-        } else if (own) {
-          x[r] = xo;
+      for (int r = 0; r < R; ++r) {
+        for (int ln = 0; ln < G; ++ln) {
+          int e = r * G + ln;
+          if (e >= d) break;
+          bool own = g.lane == ln;
+          double xo = x[r];
+          if (own) x[r] += z[r];
+          double lpp = M::logf_p(A, B, pc, s, l, g, x);
+          const double ue = G == 32 ? lane_value(uown[r], ln) : mmb_uniform(&ru, (uint32_t)e);
+          if (ue < mmb_exp(lpp - logf0)) {
+            logf0 = lpp;
+            if (own) acc[r] += ad;
+          } else if (own) {
+            x[r] = xo;
+          }
         }
       }
     }

@@ -157,6 +157,13 @@ class Engine:
             out[b] = {"updates": r[0], "full_rank": r[1], "rank_sum": r[2], "steps_sum": r[3], "redo": r[4]}
         return out
 
+    def amwg_stats(self):
+        """AMWG block updates since init_chains that ran the sequential coordinate loop
+        (mmb_amwg_stats) rather than the lane-parallel decision of every coordinate."""
+        v = (C.c_int64 * 1)()
+        self._chk(self.lib.mmb_amwg_stats(self.h, v))
+        return {"sequential_updates": v[0]}
+
     def ir_jit(self):
         """Node-IR engines: (True, info) when the specialised kernel runs (mmb_create_ir compiled
         the model with hipRTC or found it in the cache), (False, reason) for the interpreter."""

@@ -159,6 +159,36 @@ def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
     assert 0.2 < (tv[:, 2] != 0).mean() < 0.9  # alpha factor validity split: the order is not the identity
 
 
+def test_amwg_lane_parallel_path_matches_sequential(mamba, oracle, monkeypatch):
+    """samplers.h amwg_lanes decides every coordinate of the rats alpha / beta AMWG blocks at
+    once when each accept test is certain under the logpdf's rounding bound, and falls back to
+    amwg_sub!'s sequential loop otherwise.  Default, sequential-only (MMB_AMWG_EXACT=1) and a
+    2^30 times wider band (=2: many chains of a wavefront fall back while their partner does
+    not) give the same draws, values and tune as the oracle, bit for bit; by default the
+    fallback is rare."""
+    m = rats(mamba, mamba.model.rats_scheme_reference())
+    init = mamba.model.rats_init_matrix(1024)
+    iters = 120
+    out, seqn = {}, {}
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("MMB_AMWG_EXACT", mode)
+        eng = mamba.Engine(m)
+        eng.init_chains(init, seed=71)
+        d = eng.run(iters, burnin=30, thin=2)
+        out[mode] = (d, eng.values(), eng.tune())
+        seqn[mode] = eng.amwg_stats()["sequential_updates"]
+    st = oracle.new_state(m, init)
+    do = oracle.run(m, st, iters, burnin=30, thin=2, seed=71, nthreads=8)
+    for mode in out:
+        np.testing.assert_array_equal(out[mode][0], do)
+        np.testing.assert_array_equal(out[mode][1], st["values"])
+        np.testing.assert_array_equal(out[mode][2], st["tune"][:, :st["tl"]])
+    updates = 2 * init.shape[0] * iters  # alpha and beta blocks
+    assert seqn["1"] == 0  # forced: not counted as a fallback
+    assert seqn["0"] <= 0.001 * updates, seqn
+    assert 0.05 * updates < seqn["2"] < updates, seqn
+
+
 def test_restart_and_sharding(mamba, oracle):
     m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
     init = mamba.model.rats_init_ls(128, seed=3)
