@@ -196,8 +196,11 @@ struct LgHmc {
   }
 };
 
+#ifndef MMB_LG_CTL_WAVES
+#define MMB_LG_CTL_WAVES 1
+#endif
 template <class MC>
-__global__ __launch_bounds__(256) void lg_ctl_kernel(const LgArgs A, int start, int parity, int fold) {
+__global__ __launch_bounds__(256, MMB_LG_CTL_WAVES) void lg_ctl_kernel(const LgArgs A, int start, int parity, int fold) {
   // the first step visits every chain; later steps visit the chains that requested the
   // gradient just computed (slot order of the previous control kernel), so the grid and the
   // work shrink with the running chains at the end of a window

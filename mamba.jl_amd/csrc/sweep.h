@@ -78,7 +78,11 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& A) {
                          : B.adapt == MMB_ADAPT_BURNIN ? (it <= A.model_burnin) : false;
       switch (B.kind) {
         case MMB_SAMPLER_AMWG:
-          if constexpr ((KINDS >> MMB_SAMPLER_AMWG) & 1u) S::amwg(A, B, c, rn, ru, adapt, s, l, g);
+          if constexpr ((KINDS >> MMB_SAMPLER_AMWG) & 1u) {
+            MMB_PROF_START
+            S::amwg(A, B, c, rn, ru, adapt, s, l, g);
+            MMB_PROF_MARK(13, g.lane)
+          }
           break;
         case MMB_SAMPLER_AMM:
           if constexpr ((KINDS >> MMB_SAMPLER_AMM) & 1u) S::amm(A, B, c, chain, it, b, rn, ru, adapt, s, l, g, lds,
@@ -86,8 +90,10 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& A) {
           break;
         case MMB_SAMPLER_SLICE:
           if constexpr ((KINDS >> MMB_SAMPLER_SLICE) & 1u) {
+            MMB_PROF_START
             if (B.form == MMB_SLICE_UNIVARIATE) S::slice_uni(A, B, ru, s, l, g);
             else S::slice_multi(A, B, ru, s, l, g);
+            MMB_PROF_MARK(14, g.lane)
           }
           break;
         case MMB_SAMPLER_NUTS:

@@ -11,8 +11,8 @@ void mmb_prof_dump() {
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mmb_prof), sizeof h) != hipSuccess) return;
   const char* names[] = {"-", "amm:load m/fl/Mv", "amm:proposal", "amm:logf x2+accept", "amm:moments+Sigma",
                          "amm:pchol", "amm:store", "gibbs", "iteration", "count", "pchol:steps",
-                         "pchol:carry", "pchol:writeback", "-"};
-  for (int i = 1; i < 14; ++i) fprintf(stderr, "MMB_PROF %-22s %llu\n", names[i], h[i]);
+                         "pchol:carry", "pchol:writeback", "amwg", "slice", "-"};
+  for (int i = 1; i < 15; ++i) fprintf(stderr, "MMB_PROF %-22s %llu\n", names[i], h[i]);
 }
 #endif
 
