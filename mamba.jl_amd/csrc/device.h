@@ -140,8 +140,9 @@ struct SweepArgs {
   int32_t ir_amm;        // AMM scratch doubles at the start of a chain's LDS (0 without AMM)
   int32_t ir_lds;        // LDS doubles per chain
   const int32_t* cperm;  // lane-group slot -> chain (null: identity), engine.cpp order_chains
-  int32_t amwg_exact;    // MMB_AMWG_EXACT: 1 = AMWG always takes the sequential path (samplers.h
-                         // amwg), 2 = certainty band widened 2^30 times (tests: frequent fallback)
+  int32_t amwg_exact;    // MMB_AMWG_EXACT: 1 = AMWG and Slice take their sequential paths (samplers.h
+                         // amwg, slice_uni / slice_multi), 2 = AMWG certainty band widened 2^30
+                         // times (tests: frequent fallback)
 };
 
 // Block descriptors are read-only for a launch: read them through the constant address

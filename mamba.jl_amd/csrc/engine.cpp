@@ -1012,7 +1012,7 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
   A.cperm = e->cperm_identity ? nullptr : e->d_cperm;
-  {  // MMB_AMWG_EXACT=1: every AMWG update by the sequential loop; 2: wide certainty band
+  {  // MMB_AMWG_EXACT=1: AMWG and Slice updates by their sequential loops; 2: wide AMWG band
     const char* ae = std::getenv("MMB_AMWG_EXACT");
     const int v = ae ? std::atoi(ae) : 0;
     A.amwg_exact = (v == 1 || v == 2) ? v : 0;

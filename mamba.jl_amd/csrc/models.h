@@ -280,6 +280,87 @@ struct Mdl<MMB_MODEL_RATS> {
     }
     return lp;
   }
+  // Slice (Univariate) on a scalar block with its candidates evaluated four at a time
+  // (samplers.h slice_uni_cand): lanes 8q .. 8q+7 of the chain's 32 evaluate candidate q, lane
+  // l of the eight holding rats 4l .. 4l+3.  A lane sums its four leaves as ((v0 + v1) + (v2 +
+  // v3)) -- levels 0 and 1 of logf's 32-lane butterfly -- and levels 2, 3 and 4 (quad pairs,
+  // 8-lane pairs, 16-lane halves) are xor 1, xor 2 and the half-row mirror of the eight lanes:
+  // the same tree over the same leaves, so the sum is logf's bit for bit.  Everything else in
+  // slice_cand_logf is logf's code on the candidate's node values.
+  static constexpr bool SLICE_CAND = true;
+  static constexpr int SLICE_CAND_D = 2;  // scalar blocks of up to two nodes
+  struct SCtx {
+    const double* ab;  // LDS: alpha[32] | beta[32] of the chain
+    double ss;         // y's residual sum of squares (alpha, beta are not in the block)
+    unsigned tm;       // target mask as logf forms it
+  };
+  __device__ __forceinline__ static bool slice_cand_ok(const DBlock& B) {
+    return !is_vec(B.nodes[0]) && B.nn == B.d && B.d <= SLICE_CAND_D;
+  }
+  __device__ __forceinline__ static void slice_cand_prep(const SweepArgs& A, const DBlock& B, const St& s, const Lc& l,
+                                                         const Grp<G>& g, double* lds, SCtx& c) {
+    unsigned tm = 0;
+    for (int a = 0; a < B.nn; ++a) {
+      const int n = B.nodes[a];
+      tm |= (n == MMB_RATS_S2_C) ? 4u : (n == MMB_RATS_MU_ALPHA || n == MMB_RATS_S2_ALPHA) ? 1u : 2u;
+    }
+    c.tm = tm;
+    c.ss = (tm & 4u) ? g.sum(ssr_lane(A, l, s.a, s.b, g.lane)) : 0.0;
+    lds[g.lane] = s.a[0];
+    lds[32 + g.lane] = s.b[0];
+    c.ab = lds;
+    grp_sync();
+  }
+  // normsum_lane + g.sum over the 8-lane candidate group (see above); v: alpha or beta in LDS
+  __device__ __forceinline__ static double normsum_grp8(double mu, double sig, double logsig, const double* v,
+                                                        int lane) {
+    const int r0 = 4 * (lane & 7);
+    const double2 p = *(const double2*)(v + r0), q2 = *(const double2*)(v + r0 + 2);
+    const double v4[4] = {p.x, p.y, q2.x, q2.y};
+    double lf[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) lf[m] = 0.0 + (r0 + m < 30 ? d_normlogpdf(mu, sig, logsig, v4[m]) : 0.0);
+    double q = (lf[0] + lf[1]) + (lf[2] + lf[3]);
+    q += Grp<G>::template other_d<0>(q);
+    q += Grp<G>::template other_d<1>(q);
+    q += Grp<G>::template other_d<2>(q);
+    return q;
+  }
+  // logf(block) at the block vector xv[] (group-uniform values, the candidate's)
+  __device__ __forceinline__ static double slice_cand_logf(const SweepArgs& A, const DBlock& B, const St& s0,
+                                                           const SCtx& c, const double* xv, int lane) {
+    St s = s0;
+#pragma unroll
+    for (int a = 0; a < SLICE_CAND_D; ++a) {  // relist (B.nn <= SLICE_CAND_D: slice_cand_ok)
+      if (a < B.nn) {
+        const int n = B.nodes[a];
+        set_scalar(s, n, (B.transform && positive(n)) ? mmb_exp(xv[a]) : xv[a]);
+      }
+    }
+    double lp = 0.0;
+    bool stop = false;
+    for (int a = 0; a < B.nn; ++a) {
+      if (stop) continue;
+      const int n = B.nodes[a];
+      double t = positive(n) ? d_iglogpdf(A.ig_c, scalar(s, n), B.transform)
+                             : d_normlogpdf(0.0, 1000.0, mmb_log(1000.0), scalar(s, n));
+      lp += t;
+      if (!isfinite(lp)) stop = true;
+    }
+    if (stop) return lp;
+    if (c.tm & 1u) {
+      double sig = sqrt(s.s2a);
+      lp += normsum_grp8(s.mua, sig, mmb_log(sig), c.ab, lane);
+      if (!isfinite(lp)) return lp;
+    }
+    if (c.tm & 2u) {
+      double sig = sqrt(s.s2b);
+      lp += normsum_grp8(s.mub, sig, mmb_log(sig), c.ab + 32, lane);
+      if (!isfinite(lp)) return lp;
+    }
+    if (c.tm & 4u) lp += d_iso(150, sqrt(s.s2c), c.ss);
+    return lp;
+  }
   // The random draw of a conjugate block does not depend on the chain state: a Gamma(a)
   // variate for the s2 blocks (rand(InverseGamma(a, b)) = b / G, shape a fixed by the
   // model), a standard normal for the mu blocks.  The sweep kernel draws them for all
@@ -388,6 +469,9 @@ struct Mdl<MMB_MODEL_LINE> {
     }
   }
   static constexpr bool AMWG_SEP = false;  // samplers.h amwg: sequential path only
+  static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
+  static constexpr int SLICE_CAND_D = 1;
+  struct SCtx {};
   struct Prep {};
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep&,

@@ -1401,9 +1401,98 @@ struct Smp {
     const int src = (int)(threadIdx.x & 63 & ~(G - 1)) + (int)(k - w.base);
     return __shfl(w.u, src, 64);
   }
+  // slice.jl:66-92 (Univariate) with the shrink loop's candidates evaluated four at a time
+  // (models with M::SLICE_CAND: lanes 8q .. 8q+7 of the chain evaluate candidate q).  Given that
+  // every earlier candidate was rejected, the candidates of a coordinate are fixed in advance:
+  // candidate j = lo + (up - lo) * u_j, then lo or up moves to it by its side of the current
+  // value -- the loop's arithmetic on its uniforms, independent of the logpdf values.  A round
+  // forms the next four on every lane, evaluates them at once (exact logf values: the model's
+  // evaluator sums the same tree), and takes the first that the loop would accept; the uniform
+  // index, the logf0 carried to the next coordinate and the overflow case follow the loop.  The
+  // draws are the sequential loop's, bit for bit.
+  __device__ __forceinline__ static void slice_uni_cand(const SweepArgs& A, const DBlock& B, const mmb_rng& ru,
+                                                        St& s, const Lc& l, const Grp<G>& g, double* lds) {
+    constexpr int SD = M::SLICE_CAND_D;
+    static_assert(MMB_SLICE_MAX_SHRINK % 4 == 0, "rounds of four candidates end at the cap");
+    const int d = B.d;
+    double x[R];
+    M::unlist(B, s, g.lane, x);
+    double logf0 = M::logf(A, B, s, l, g, x);
+    double lo = 0.0, up = 0.0;
+    if (g.lane < d) {
+      const double w = width(B, g.lane);
+      lo = x[0] - w * mmb_uniform(&ru, (uint32_t)g.lane);
+      up = lo + w;
+    }
+    typename M::SCtx cx;
+    M::slice_cand_prep(A, B, s, l, g, lds, cx);
+    double xu[SD], lou[SD], upu[SD];  // element values and intervals, group-uniform
+#pragma unroll
+    for (int a = 0; a < SD; ++a) {
+      xu[a] = a < d ? g.bcast(x[0], a) : 0.0;
+      lou[a] = a < d ? g.bcast(lo, a) : 0.0;
+      upu[a] = a < d ? g.bcast(up, a) : 0.0;
+    }
+    uint32_t k = (uint32_t)d;
+    UWin uw{0.0, 0xffffffffu - (uint32_t)G};
+    const int q = (g.lane >> 3) & 3;
+    const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
+    for (int e = 0; e < d; ++e) {
+      const double p0 = logf0 + mmb_log(uwin_next(ru, uw, k++, g));
+      double xo = xu[0], lo_ = lou[0], up_ = upu[0];
+#pragma unroll
+      for (int a = 1; a < SD; ++a)
+        if (a == e) { xo = xu[a]; lo_ = lou[a]; up_ = upu[a]; }
+      double xn = 0.0, lfn = 0.0;
+      // candidate j (from 1) takes uniform k + j - 1
+      for (uint32_t j0 = 0;; j0 += 4) {
+        double cand[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const double cv = lo_ + (up_ - lo_) * uwin_next(ru, uw, k + j0 + (uint32_t)t, g);
+          cand[t] = cv;
+          if (cv < xo) lo_ = cv;
+          else up_ = cv;
+        }
+        const double mine = q == 0 ? cand[0] : q == 1 ? cand[1] : q == 2 ? cand[2] : cand[3];
+        double xv[SD];
+#pragma unroll
+        for (int a = 0; a < SD; ++a) xv[a] = a == e ? mine : xu[a];
+        const double lp = M::slice_cand_logf(A, B, s, cx, xv, g.lane);
+        const bool hit = !(lp < p0) && j0 + (uint32_t)q + 1u <= (uint32_t)MMB_SLICE_MAX_SHRINK;
+        const uint64_t bal = __ballot(hit && (g.lane & 7) == 0);
+        const uint32_t hb = (uint32_t)(bal >> gbase) & 0x01010101u;  // candidate q -> bit 8q
+        if (hb != 0u) {
+          const int qs = __builtin_ctz(hb) >> 3;
+          xn = qs == 0 ? cand[0] : qs == 1 ? cand[1] : qs == 2 ? cand[2] : cand[3];
+          lfn = __shfl(lp, gbase + 8 * qs, 64);
+          k += j0 + (uint32_t)qs + 1u;
+          break;
+        }
+        if (j0 + 4u >= (uint32_t)MMB_SLICE_MAX_SHRINK) {  // every candidate up to the cap rejected:
+          xn = lo_ + (up_ - lo_) * uwin_next(ru, uw, k + j0 + 4u, g);  // the loop's last draw
+          lfn = __shfl(lp, gbase + 24, 64);                             // logf of the cap-th
+          k += j0 + 5u;
+          slice_overflow(A, g);
+          break;
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < SD; ++a) xu[a] = a == e ? xn : xu[a];
+      logf0 = lfn;
+      if (g.lane == e) x[0] = xn;
+    }
+    M::relist(B, s, g, x);
+  }
   // slice.jl:66-92 (Univariate)
   __device__ __forceinline__ static void slice_uni(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
-                                   const Lc& l, const Grp<G>& g) {
+                                   const Lc& l, const Grp<G>& g, double* lds) {
+    if constexpr (M::SLICE_CAND && G == 32 && R == 1) {
+      if (A.amwg_exact != 1 && M::slice_cand_ok(B)) {
+        slice_uni_cand(A, B, ru, s, l, g, lds);
+        return;
+      }
+    }
     const int d = B.d;
     double x[R], lo[R], up[R];
     M::unlist(B, s, g.lane, x);
@@ -1450,9 +1539,96 @@ struct Smp {
     }
     M::relist(B, s, g, x);
   }
+  // slice.jl:95-117 (Multivariate), candidates four at a time as slice_uni_cand: candidate 1 is
+  // w u + lo per element, candidate j > 1 moves each lo / up to candidate j - 1's element by its
+  // side of the current value and draws lo + (up - lo) u, uniforms 1 + 2d + (j - 2) d + e
+  __device__ __forceinline__ static void slice_multi_cand(const SweepArgs& A, const DBlock& B, const mmb_rng& ru,
+                                                          St& s, const Lc& l, const Grp<G>& g, double* lds) {
+    constexpr int SD = M::SLICE_CAND_D;
+    const int d = B.d;
+    double v[R];
+    M::unlist(B, s, g.lane, v);
+    UWin uw{0.0, 0xffffffffu - (uint32_t)G};
+    const double p0 = M::logf(A, B, s, l, g, v) + mmb_log(uwin_next(ru, uw, 0u, g));
+    typename M::SCtx cx;
+    M::slice_cand_prep(A, B, s, l, g, lds, cx);
+    double vu[SD], lo[SD], up[SD], x1[SD];
+#pragma unroll
+    for (int a = 0; a < SD; ++a) {
+      vu[a] = a < d ? g.bcast(v[0], a) : 0.0;
+      lo[a] = up[a] = x1[a] = 0.0;
+      if (a < d) {
+        const double w = width(B, a);
+        lo[a] = vu[a] - w * uwin_next(ru, uw, 1u + (uint32_t)a, g);
+        up[a] = lo[a] + w;
+        x1[a] = w * uwin_next(ru, uw, 1u + (uint32_t)d + (uint32_t)a, g) + lo[a];
+      }
+    }
+    const int q = (g.lane >> 3) & 3;
+    const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
+    double prev[SD], xn[SD];
+    // candidate j > 1 from candidate j - 1 (the loop's shrink and redraw)
+    auto next = [&](const double* pv, uint32_t j, double* out) __attribute__((always_inline)) {
+      const uint32_t kk = 1u + 2u * (uint32_t)d + (j - 2u) * (uint32_t)d;
+#pragma unroll
+      for (int a = 0; a < SD; ++a) {
+        if (a < d) {
+          if (pv[a] < vu[a]) lo[a] = pv[a];
+          else up[a] = pv[a];
+          out[a] = lo[a] + (up[a] - lo[a]) * uwin_next(ru, uw, kk + (uint32_t)a, g);
+        } else {
+          out[a] = 0.0;
+        }
+      }
+    };
+    for (uint32_t j0 = 0;; j0 += 4) {
+      double cand[4][SD];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (j0 + (uint32_t)t == 0u) {
+#pragma unroll
+          for (int a = 0; a < SD; ++a) cand[t][a] = x1[a];
+        } else {
+          next(t == 0 ? prev : cand[t - 1], j0 + (uint32_t)t + 1u, cand[t]);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < SD; ++a) prev[a] = cand[3][a];
+      double xv[SD];
+#pragma unroll
+      for (int a = 0; a < SD; ++a) xv[a] = q == 0 ? cand[0][a] : q == 1 ? cand[1][a] : q == 2 ? cand[2][a] : cand[3][a];
+      const double lp = M::slice_cand_logf(A, B, s, cx, xv, g.lane);
+      const bool hit = !(lp < p0) && j0 + (uint32_t)q + 1u <= (uint32_t)MMB_SLICE_MAX_SHRINK;
+      const uint64_t bal = __ballot(hit && (g.lane & 7) == 0);
+      const uint32_t hb = (uint32_t)(bal >> gbase) & 0x01010101u;
+      if (hb != 0u) {
+        const int qs = __builtin_ctz(hb) >> 3;
+#pragma unroll
+        for (int a = 0; a < SD; ++a) xn[a] = qs == 0 ? cand[0][a] : qs == 1 ? cand[1][a] : qs == 2 ? cand[2][a] : cand[3][a];
+        break;
+      }
+      if (j0 + 4u >= (uint32_t)MMB_SLICE_MAX_SHRINK) {  // the cap: the loop's last shrink and draw
+        next(prev, j0 + 5u, xn);
+        slice_overflow(A, g);
+        break;
+      }
+    }
+    double x[R];
+    x[0] = 0.0;
+#pragma unroll
+    for (int a = 0; a < SD; ++a)
+      if (g.lane == a && a < d) x[0] = xn[a];
+    M::relist(B, s, g, x);
+  }
   // slice.jl:95-117 (Multivariate)
   __device__ __forceinline__ static void slice_multi(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
-                                     const Lc& l, const Grp<G>& g) {
+                                     const Lc& l, const Grp<G>& g, double* lds) {
+    if constexpr (M::SLICE_CAND && G == 32 && R == 1) {
+      if (A.amwg_exact != 1 && M::slice_cand_ok(B)) {
+        slice_multi_cand(A, B, ru, s, l, g, lds);
+        return;
+      }
+    }
     const int d = B.d;
     double v[R], x[R], lo[R], up[R];
     M::unlist(B, s, g.lane, v);

@@ -91,8 +91,8 @@ __device__ __forceinline__ void sweep_body(const SweepArgs& A) {
         case MMB_SAMPLER_SLICE:
           if constexpr ((KINDS >> MMB_SAMPLER_SLICE) & 1u) {
             MMB_PROF_START
-            if (B.form == MMB_SLICE_UNIVARIATE) S::slice_uni(A, B, ru, s, l, g);
-            else S::slice_multi(A, B, ru, s, l, g);
+            if (B.form == MMB_SLICE_UNIVARIATE) S::slice_uni(A, B, ru, s, l, g, lds);
+            else S::slice_multi(A, B, ru, s, l, g, lds);
             MMB_PROF_MARK(14, g.lane)
           }
           break;

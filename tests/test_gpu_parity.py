@@ -162,7 +162,9 @@ def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
 def test_amwg_lane_parallel_path_matches_sequential(mamba, oracle, monkeypatch):
     """samplers.h amwg_lanes decides every coordinate of the rats alpha / beta AMWG blocks at
     once when each accept test is certain under the logpdf's rounding bound, and falls back to
-    amwg_sub!'s sequential loop otherwise.  Default, sequential-only (MMB_AMWG_EXACT=1) and a
+    amwg_sub!'s sequential loop otherwise; the scalar-block Slice updates evaluate their shrink
+    candidates four at a time (slice_uni_cand / slice_multi_cand).  Default, sequential-only
+    for both (MMB_AMWG_EXACT=1) and a
     2^30 times wider band (=2: many chains of a wavefront fall back while their partner does
     not) give the same draws, values and tune as the oracle, bit for bit; by default the
     fallback is rare."""
@@ -187,6 +189,23 @@ def test_amwg_lane_parallel_path_matches_sequential(mamba, oracle, monkeypatch):
     assert seqn["1"] == 0  # forced: not counted as a fallback
     assert seqn["0"] <= 0.001 * updates, seqn
     assert 0.05 * updates < seqn["2"] < updates, seqn
+
+
+@pytest.mark.parametrize("which", ["multi_s2_c", "uni_mu_alpha"])
+def test_rats_slice_overflow_is_an_error(mamba, which):
+    """The rats scalar-block Slice evaluates its shrink candidates four at a time
+    (samplers.h slice_uni_cand / slice_multi_cand) and stops at the same cap as the sequential
+    loop: an infinite width (every candidate NaN) is reported as MMB_E_STATE."""
+    S = mamba.model.rats_scheme_reference()
+    if which == "multi_s2_c":
+        S[0] = mamba.Slice("s2_c", np.inf)
+    else:
+        S[2] = mamba.Slice(["mu_alpha", "s2_alpha"], [np.inf, 10.0], mamba.Univariate)
+    m = rats(mamba, S)
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_matrix(3), seed=2)
+    with pytest.raises(RuntimeError, match=r"error -4 .*Slice: 3 update\(s\) in iterations 1\.\.1"):
+        eng.run(1, burnin=0, thin=1)
 
 
 def test_restart_and_sharding(mamba, oracle):
