@@ -325,6 +325,7 @@ def main():
     eng.reserve_draws(args.steps // thin + 1)
     nuts_before = eng.nuts_stats() if nuts else None
     amm_before = eng.amm_stats()
+    amwg_before = eng.amwg_stats()["sequential_updates"]
     barrier()
     t0 = time.perf_counter()
     eng.run(args.steps, burnin=tburn, thin=thin, model_burnin=mburn, draws=False, keep_device=True,
@@ -345,6 +346,10 @@ def main():
                          f"window's {ms_per_step:.4f} ms by more than 5 % — timing is inconsistent")
     grads_timed = eng.grad_evals() if nuts else 0  # (the counter restarts with every mmb_run)
     amm_timed = amm_window(model, amm_before, eng.amm_stats())
+    # AMWG block updates of the window that fell back to amwg_sub!'s sequential loop (the
+    # lane-parallel decision was not certain for some coordinate; samplers.h amwg_lanes)
+    amwg_seq = eng.amwg_stats()["sequential_updates"] - amwg_before
+    n_amwg = sum(1 for s in model.samplers if getattr(s, "kind", None) == mb.abi.MMB_SAMPLER_AMWG)
     nuts_timed = None
     if nuts:
         after = eng.nuts_stats()
@@ -491,6 +496,8 @@ def main():
             out["config"]["amm_adapt"] = "all"
     if amm_timed:
         out["config"]["amm"] = amm_timed
+    if n_amwg:
+        out["config"]["amwg"] = {"block_updates": n_amwg * K * args.steps, "sequential_fallbacks": int(amwg_seq)}
     if args.workload.endswith("_ir"):
         # node IR: the specialised kernel (mmb_create_ir -> hipRTC, csrc/ir_jit.cpp) or the interpreter
         jit, info = eng.ir_jit()
