@@ -205,6 +205,7 @@ struct Mdl<MMB_MODEL_IR> {
   static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
   static constexpr int SLICE_CAND_D = 1;
   struct SCtx {};
+  struct SMemo {};
   struct Prep {};
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   // logpdf!(m, x, block, transform)

@@ -289,6 +289,12 @@ struct Mdl<MMB_MODEL_RATS> {
   // slice_cand_logf is logf's code on the candidate's node values.
   static constexpr bool SLICE_CAND = true;
   static constexpr int SLICE_CAND_D = 2;  // scalar blocks of up to two nodes
+#ifndef MMB_SLICE_NC
+#define MMB_SLICE_NC 4
+#endif
+  // candidates per round: NC groups of 32 / NC lanes, NC leaves (rats) per lane
+  static constexpr int SLICE_NC = MMB_SLICE_NC;
+  static_assert(SLICE_NC == 4 || SLICE_NC == 8, "4 or 8 candidates per round");
   struct SCtx {
     const double* ab;  // LDS: alpha[32] | beta[32] of the chain
     double ss;         // y's residual sum of squares (alpha, beta are not in the block)
@@ -311,24 +317,59 @@ struct Mdl<MMB_MODEL_RATS> {
     c.ab = lds;
     grp_sync();
   }
-  // normsum_lane + g.sum over the 8-lane candidate group (see above); v: alpha or beta in LDS
+  // normsum_lane + g.sum over the candidate group (see above); v: alpha or beta in LDS.  NC = 8:
+  // groups of four lanes with eight leaves each, levels 0-2 in the lane, 3-4 by xor 1 and xor 2.
   __device__ __forceinline__ static double normsum_grp8(double mu, double sig, double logsig, const double* v,
                                                         int lane) {
-    const int r0 = 4 * (lane & 7);
-    const double2 p = *(const double2*)(v + r0), q2 = *(const double2*)(v + r0 + 2);
-    const double v4[4] = {p.x, p.y, q2.x, q2.y};
-    double lf[4];
+    constexpr int L = SLICE_NC, LPC = 32 / SLICE_NC;
+    const int r0 = L * (lane & (LPC - 1));
+    double lf[L];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) lf[m] = 0.0 + (r0 + m < 30 ? d_normlogpdf(mu, sig, logsig, v4[m]) : 0.0);
+    for (int m = 0; m < L; m += 2) {
+      const double2 p = *(const double2*)(v + r0 + m);
+      lf[m] = 0.0 + (r0 + m < 30 ? d_normlogpdf(mu, sig, logsig, p.x) : 0.0);
+      lf[m + 1] = 0.0 + (r0 + m + 1 < 30 ? d_normlogpdf(mu, sig, logsig, p.y) : 0.0);
+    }
     double q = (lf[0] + lf[1]) + (lf[2] + lf[3]);
+    if constexpr (L == 8) q = q + ((lf[4] + lf[5]) + (lf[6] + lf[7]));
     q += Grp<G>::template other_d<0>(q);
     q += Grp<G>::template other_d<1>(q);
-    q += Grp<G>::template other_d<2>(q);
+    if constexpr (LPC == 8) q += Grp<G>::template other_d<2>(q);
     return q;
   }
+  // The pieces of slice_cand_logf that only depend on one node value -- each block node's prior
+  // term, the target variance's square root and log -- memoised per lane by the bits of that
+  // value: the nodes other than the coordinate being sampled keep their values through all of
+  // the coordinate's candidates, so their priors (a log and a division for a variance node) and,
+  // for a mean coordinate, the target scale (a square root and a log) are formed once.  A hit
+  // returns the value the same function gave for the same input bits; a NaN input is never
+  // cached (the keys start as a NaN pattern).
+  struct SMemo {
+    uint64_t pk[SLICE_CAND_D];
+    double pt[SLICE_CAND_D];
+    uint64_t sk;
+    double sg, lsg;
+    __device__ __forceinline__ SMemo() : sk(0x7ff0000000000001ull), sg(0.0), lsg(0.0) {
+#pragma unroll
+      for (int a = 0; a < SLICE_CAND_D; ++a) { pk[a] = 0x7ff0000000000001ull; pt[a] = 0.0; }
+    }
+    __device__ __forceinline__ void scale(double var, double& sig, double& lsig) {
+      const uint64_t vb = mmb_d2u(var);
+      if (vb == sk && var == var) {
+        sig = sg;
+        lsig = lsg;
+      } else {
+        sig = sqrt(var);
+        lsig = mmb_log(sig);
+        sk = vb;
+        sg = sig;
+        lsg = lsig;
+      }
+    }
+  };
   // logf(block) at the block vector xv[] (group-uniform values, the candidate's)
   __device__ __forceinline__ static double slice_cand_logf(const SweepArgs& A, const DBlock& B, const St& s0,
-                                                           const SCtx& c, const double* xv, int lane) {
+                                                           const SCtx& c, const double* xv, int lane, SMemo& mm) {
     St s = s0;
 #pragma unroll
     for (int a = 0; a < SLICE_CAND_D; ++a) {  // relist (B.nn <= SLICE_CAND_D: slice_cand_ok)
@@ -339,23 +380,34 @@ struct Mdl<MMB_MODEL_RATS> {
     }
     double lp = 0.0;
     bool stop = false;
-    for (int a = 0; a < B.nn; ++a) {
-      if (stop) continue;
+#pragma unroll
+    for (int a = 0; a < SLICE_CAND_D; ++a) {
+      if (a >= B.nn || stop) continue;
       const int n = B.nodes[a];
-      double t = positive(n) ? d_iglogpdf(A.ig_c, scalar(s, n), B.transform)
-                             : d_normlogpdf(0.0, 1000.0, mmb_log(1000.0), scalar(s, n));
+      const double v = scalar(s, n);
+      const uint64_t vb = mmb_d2u(v);
+      double t;
+      if (vb == mm.pk[a] && v == v) {
+        t = mm.pt[a];
+      } else {
+        t = positive(n) ? d_iglogpdf(A.ig_c, v, B.transform) : d_normlogpdf(0.0, 1000.0, mmb_log(1000.0), v);
+        mm.pk[a] = vb;
+        mm.pt[a] = t;
+      }
       lp += t;
       if (!isfinite(lp)) stop = true;
     }
     if (stop) return lp;
     if (c.tm & 1u) {
-      double sig = sqrt(s.s2a);
-      lp += normsum_grp8(s.mua, sig, mmb_log(sig), c.ab, lane);
+      double sig, lsig;
+      mm.scale(s.s2a, sig, lsig);
+      lp += normsum_grp8(s.mua, sig, lsig, c.ab, lane);
       if (!isfinite(lp)) return lp;
     }
     if (c.tm & 2u) {
-      double sig = sqrt(s.s2b);
-      lp += normsum_grp8(s.mub, sig, mmb_log(sig), c.ab + 32, lane);
+      double sig, lsig;
+      mm.scale(s.s2b, sig, lsig);
+      lp += normsum_grp8(s.mub, sig, lsig, c.ab + 32, lane);
       if (!isfinite(lp)) return lp;
     }
     if (c.tm & 4u) lp += d_iso(150, sqrt(s.s2c), c.ss);
@@ -472,6 +524,7 @@ struct Mdl<MMB_MODEL_LINE> {
   static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
   static constexpr int SLICE_CAND_D = 1;
   struct SCtx {};
+  struct SMemo {};
   struct Prep {};
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   __device__ __forceinline__ static double logf_p(const SweepArgs& A, const DBlock& B, const Prep&,

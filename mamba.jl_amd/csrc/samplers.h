@@ -1413,7 +1413,9 @@ struct Smp {
   __device__ __forceinline__ static void slice_uni_cand(const SweepArgs& A, const DBlock& B, const mmb_rng& ru,
                                                         St& s, const Lc& l, const Grp<G>& g, double* lds) {
     constexpr int SD = M::SLICE_CAND_D;
-    static_assert(MMB_SLICE_MAX_SHRINK % 4 == 0, "rounds of four candidates end at the cap");
+    constexpr int NC = M::SLICE_NC, LPC = 32 / NC;  // candidates per round, lanes per candidate
+    constexpr uint32_t LEAD = NC == 4 ? 0x01010101u : 0x11111111u;  // group leaders' ballot bits
+    static_assert(MMB_SLICE_MAX_SHRINK % NC == 0, "rounds of candidates end at the cap");
     const int d = B.d;
     double x[R];
     M::unlist(B, s, g.lane, x);
@@ -1426,6 +1428,7 @@ struct Smp {
     }
     typename M::SCtx cx;
     M::slice_cand_prep(A, B, s, l, g, lds, cx);
+    typename M::SMemo memo;
     double xu[SD], lou[SD], upu[SD];  // element values and intervals, group-uniform
 #pragma unroll
     for (int a = 0; a < SD; ++a) {
@@ -1435,7 +1438,7 @@ struct Smp {
     }
     uint32_t k = (uint32_t)d;
     UWin uw{0.0, 0xffffffffu - (uint32_t)G};
-    const int q = (g.lane >> 3) & 3;
+    const int q = g.lane / LPC;
     const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
     for (int e = 0; e < d; ++e) {
       const double p0 = logf0 + mmb_log(uwin_next(ru, uw, k++, g));
@@ -1445,34 +1448,38 @@ struct Smp {
         if (a == e) { xo = xu[a]; lo_ = lou[a]; up_ = upu[a]; }
       double xn = 0.0, lfn = 0.0;
       // candidate j (from 1) takes uniform k + j - 1
-      for (uint32_t j0 = 0;; j0 += 4) {
-        double cand[4];
+      for (uint32_t j0 = 0;; j0 += NC) {
+        double cand[NC];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < NC; ++t) {
           const double cv = lo_ + (up_ - lo_) * uwin_next(ru, uw, k + j0 + (uint32_t)t, g);
           cand[t] = cv;
           if (cv < xo) lo_ = cv;
           else up_ = cv;
         }
-        const double mine = q == 0 ? cand[0] : q == 1 ? cand[1] : q == 2 ? cand[2] : cand[3];
+        double mine = cand[0];
+#pragma unroll
+        for (int t = 1; t < NC; ++t) mine = q == t ? cand[t] : mine;
         double xv[SD];
 #pragma unroll
         for (int a = 0; a < SD; ++a) xv[a] = a == e ? mine : xu[a];
-        const double lp = M::slice_cand_logf(A, B, s, cx, xv, g.lane);
+        const double lp = M::slice_cand_logf(A, B, s, cx, xv, g.lane, memo);
         const bool hit = !(lp < p0) && j0 + (uint32_t)q + 1u <= (uint32_t)MMB_SLICE_MAX_SHRINK;
-        const uint64_t bal = __ballot(hit && (g.lane & 7) == 0);
-        const uint32_t hb = (uint32_t)(bal >> gbase) & 0x01010101u;  // candidate q -> bit 8q
+        const uint64_t bal = __ballot(hit && (g.lane & (LPC - 1)) == 0);
+        const uint32_t hb = (uint32_t)(bal >> gbase) & LEAD;  // candidate q -> bit LPC q
         if (hb != 0u) {
-          const int qs = __builtin_ctz(hb) >> 3;
-          xn = qs == 0 ? cand[0] : qs == 1 ? cand[1] : qs == 2 ? cand[2] : cand[3];
-          lfn = __shfl(lp, gbase + 8 * qs, 64);
+          const int qs = __builtin_ctz(hb) / LPC;
+          xn = cand[0];
+#pragma unroll
+          for (int t = 1; t < NC; ++t) xn = qs == t ? cand[t] : xn;
+          lfn = __shfl(lp, gbase + LPC * qs, 64);
           k += j0 + (uint32_t)qs + 1u;
           break;
         }
-        if (j0 + 4u >= (uint32_t)MMB_SLICE_MAX_SHRINK) {  // every candidate up to the cap rejected:
-          xn = lo_ + (up_ - lo_) * uwin_next(ru, uw, k + j0 + 4u, g);  // the loop's last draw
-          lfn = __shfl(lp, gbase + 24, 64);                             // logf of the cap-th
-          k += j0 + 5u;
+        if (j0 + (uint32_t)NC >= (uint32_t)MMB_SLICE_MAX_SHRINK) {  // every candidate up to the cap rejected:
+          xn = lo_ + (up_ - lo_) * uwin_next(ru, uw, k + j0 + (uint32_t)NC, g);  // the loop's last draw
+          lfn = __shfl(lp, gbase + LPC * (NC - 1), 64);                           // logf of the cap-th
+          k += j0 + (uint32_t)NC + 1u;
           slice_overflow(A, g);
           break;
         }
@@ -1552,6 +1559,7 @@ struct Smp {
     const double p0 = M::logf(A, B, s, l, g, v) + mmb_log(uwin_next(ru, uw, 0u, g));
     typename M::SCtx cx;
     M::slice_cand_prep(A, B, s, l, g, lds, cx);
+    typename M::SMemo memo;
     double vu[SD], lo[SD], up[SD], x1[SD];
 #pragma unroll
     for (int a = 0; a < SD; ++a) {
@@ -1564,7 +1572,9 @@ struct Smp {
         x1[a] = w * uwin_next(ru, uw, 1u + (uint32_t)d + (uint32_t)a, g) + lo[a];
       }
     }
-    const int q = (g.lane >> 3) & 3;
+    constexpr int NC = M::SLICE_NC, LPC = 32 / NC;
+    constexpr uint32_t LEAD = NC == 4 ? 0x01010101u : 0x11111111u;
+    const int q = g.lane / LPC;
     const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
     double prev[SD], xn[SD];
     // candidate j > 1 from candidate j - 1 (the loop's shrink and redraw)
@@ -1581,10 +1591,10 @@ struct Smp {
         }
       }
     };
-    for (uint32_t j0 = 0;; j0 += 4) {
-      double cand[4][SD];
+    for (uint32_t j0 = 0;; j0 += NC) {
+      double cand[NC][SD];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < NC; ++t) {
         if (j0 + (uint32_t)t == 0u) {
 #pragma unroll
           for (int a = 0; a < SD; ++a) cand[t][a] = x1[a];
@@ -1593,22 +1603,30 @@ struct Smp {
         }
       }
 #pragma unroll
-      for (int a = 0; a < SD; ++a) prev[a] = cand[3][a];
+      for (int a = 0; a < SD; ++a) prev[a] = cand[NC - 1][a];
       double xv[SD];
 #pragma unroll
-      for (int a = 0; a < SD; ++a) xv[a] = q == 0 ? cand[0][a] : q == 1 ? cand[1][a] : q == 2 ? cand[2][a] : cand[3][a];
-      const double lp = M::slice_cand_logf(A, B, s, cx, xv, g.lane);
-      const bool hit = !(lp < p0) && j0 + (uint32_t)q + 1u <= (uint32_t)MMB_SLICE_MAX_SHRINK;
-      const uint64_t bal = __ballot(hit && (g.lane & 7) == 0);
-      const uint32_t hb = (uint32_t)(bal >> gbase) & 0x01010101u;
-      if (hb != 0u) {
-        const int qs = __builtin_ctz(hb) >> 3;
+      for (int a = 0; a < SD; ++a) {
+        xv[a] = cand[0][a];
 #pragma unroll
-        for (int a = 0; a < SD; ++a) xn[a] = qs == 0 ? cand[0][a] : qs == 1 ? cand[1][a] : qs == 2 ? cand[2][a] : cand[3][a];
+        for (int t = 1; t < NC; ++t) xv[a] = q == t ? cand[t][a] : xv[a];
+      }
+      const double lp = M::slice_cand_logf(A, B, s, cx, xv, g.lane, memo);
+      const bool hit = !(lp < p0) && j0 + (uint32_t)q + 1u <= (uint32_t)MMB_SLICE_MAX_SHRINK;
+      const uint64_t bal = __ballot(hit && (g.lane & (LPC - 1)) == 0);
+      const uint32_t hb = (uint32_t)(bal >> gbase) & LEAD;
+      if (hb != 0u) {
+        const int qs = __builtin_ctz(hb) / LPC;
+#pragma unroll
+        for (int a = 0; a < SD; ++a) {
+          xn[a] = cand[0][a];
+#pragma unroll
+          for (int t = 1; t < NC; ++t) xn[a] = qs == t ? cand[t][a] : xn[a];
+        }
         break;
       }
-      if (j0 + 4u >= (uint32_t)MMB_SLICE_MAX_SHRINK) {  // the cap: the loop's last shrink and draw
-        next(prev, j0 + 5u, xn);
+      if (j0 + (uint32_t)NC >= (uint32_t)MMB_SLICE_MAX_SHRINK) {  // the cap: the loop's last shrink and draw
+        next(prev, j0 + (uint32_t)NC + 1u, xn);
         slice_overflow(A, g);
         break;
       }
