@@ -42,7 +42,7 @@ typedef __UINTPTR_TYPE__ uintptr_t;
 extern "C" {
 #endif
 
-#define MMB_ABI_VERSION 8
+#define MMB_ABI_VERSION 9
 #define MMB_MAX_BLOCKS 8
 #define MMB_MAX_NODES_PER_BLOCK 4
 
@@ -367,9 +367,26 @@ int mmb_amm_stats(mmb_engine* e, int64_t* out /* MMB_MAX_BLOCKS x MMB_AMM_STATS 
 /* AMWG path counter since init_chains: out[0] = block updates that ran amwg_sub! one coordinate
  * at a time (samplers.h amwg) instead of the lane-parallel decision of every coordinate, which
  * is taken when each coordinate's accept test is certain under the logpdf's rounding bound
- * (rats alpha / beta; the environment variable MMB_AMWG_EXACT=1 forces the sequential loop).
+ * (rats alpha / beta; the environment variable MMB_AMWG_EXACT=1 forces the sequential loop,
+ * MMB_SLICE_EXACT=1 the one-candidate-at-a-time Slice shrink loop of the rats scalar blocks).
  * Both paths give the same draws; diagnostics only. */
 int mmb_amwg_stats(mmb_engine* e, int64_t* out /* 1 */);
+
+/* The lane-group slot -> chain table the last window ran with (K entries; the identity when
+ * no ordering applies).  The 32-lane sweep kernels (rats, node IR) pair chains whose pivoted
+ * Cholesky stops alike in one wavefront; the table is a stable sort of the chains by their
+ * AMM blocks' factor-valid flags, computed on the device before each window.  Results do not
+ * depend on it (every chain keeps its own state, draws column and Philox id); diagnostics. */
+int mmb_chain_order(mmb_engine* e, int32_t* slot_to_chain);
+
+/* Diagnostics: the device's 32-lane pivoted Cholesky of the AMM update (cholfact(Hermitian(S),
+ * :U, Val{true}) = LAPACK dpstf2 for n < 64, amm.jl:87) on n caller-supplied d x d matrices,
+ * 1 <= d <= 30, packed lower triangle S[c][tri(i) + k] (i >= k, 480 doubles per matrix).  Out per
+ * matrix: info[c] = {rank, redone} (redone: the optimistic pass was redone by the checked
+ * one), pos[c][32] each element's pivot position (-1 past d) and, on full rank, L[c][480] the
+ * factor in position form: element e's row at tri(pos[e]) + k, k = 0..pos[e].  Runs on `device`
+ * outside any engine. */
+int mmb_debug_pchol(int device, int64_t n, int d, const double* S, double* L, int32_t* pos, int32_t* info);
 
 #ifdef __cplusplus
 }

@@ -114,6 +114,11 @@ function amwg_stats(e)
   out = zeros(Int64, 1)
   check(ccall((:mmb_amwg_stats, libmambahip), Cint, (Ptr{Void}, Ptr{Int64}), e, out), e); out[1]
 end
+# the slot -> chain table of the last window (wavefront pairing; results do not depend on it)
+function chain_order(e, K)
+  out = zeros(Int32, K)
+  check(ccall((:mmb_chain_order, libmambahip), Cint, (Ptr{Void}, Ptr{Int32}), e, out), e); out
+end
 function ir_jit_info(e)
   buf = zeros(UInt8, 4096)
   r = ccall((:mmb_ir_jit_info, libmambahip), Cint, (Ptr{Void}, Ptr{UInt8}, Int64), e, buf, length(buf))

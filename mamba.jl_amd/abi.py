@@ -14,7 +14,7 @@ MMB_MAX_NODES_PER_BLOCK = 4
 MMB_MODEL_LINE, MMB_MODEL_RATS, MMB_MODEL_LOGISTIC, MMB_MODEL_IR = 1, 2, 3, 4
 MMB_SAMPLER_AMWG, MMB_SAMPLER_AMM, MMB_SAMPLER_NUTS, MMB_SAMPLER_SLICE, MMB_SAMPLER_GIBBS = 1, 2, 3, 4, 5
 MMB_SAMPLER_HMC, MMB_SAMPLER_MALA = 6, 7
-MMB_ABI_VERSION = 8
+MMB_ABI_VERSION = 9
 MMB_GRAD_DEFAULT, MMB_GRAD_FORWARD, MMB_GRAD_ANALYTIC = 0, 1, 2
 MMB_SUMMARY_FIELDS, MMB_ORDER_MAX_TARGETS = 10, 16
 MMB_ADAPT_ALL, MMB_ADAPT_BURNIN, MMB_ADAPT_NONE = 0, 1, 2
@@ -116,6 +116,9 @@ def _declare(lib):
         "mmb_nuts_stats": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_amm_stats": (C.c_int, [P, C.POINTER(I64)]),
         "mmb_amwg_stats": (C.c_int, [P, C.POINTER(I64)]),
+        "mmb_chain_order": (C.c_int, [P, C.POINTER(C.c_int32)]),
+        "mmb_debug_pchol": (C.c_int, [C.c_int, I64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
         "mmb_ir_jit_info": (C.c_int, [P, C.c_char_p, I64]),
         "mmb_ir_jit_prebuild": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_char_p, I64]),
         "mmb_ir_jit_source_text": (C.c_int, [C.POINTER(ModelSpec), C.POINTER(IrModel), C.c_char_p, I64]),
@@ -154,6 +157,35 @@ def check(rc, eng=None):
         raise RuntimeError(f"mamba_hip error {rc} ({ERRORS.get(rc, '?')}): "
                            f"{msg.decode() if msg else ''}")
     return rc
+
+
+def debug_pchol(S, device=0):
+    """mmb_debug_pchol: the device's 32-lane pivoted Cholesky (samplers.h pchol32, the AMM update's
+    cholfact(Hermitian(S), :U, Val{true})) on matrices S [n, d, d] (lower triangles read).  Returns
+    (rank [n], redone [n], L [n, d, d] with L[c, e, k] = element e's factor entry at step k (zero
+    unless full rank), piv [n, d] the pivot order)."""
+    import numpy as np
+    S = np.asarray(S, dtype=np.float64)
+    n, d = S.shape[0], S.shape[1]
+    tri = lambda i: i * (i + 1) // 2  # noqa: E731
+    P = np.zeros((n, 480))
+    for i in range(d):
+        P[:, tri(i):tri(i) + i + 1] = S[:, i, :i + 1]
+    Lp = np.zeros((n, 480))
+    pos = np.zeros((n, 32), dtype=np.int32)
+    info = np.zeros((n, 2), dtype=np.int32)
+    i32 = C.POINTER(C.c_int32)
+    check(lib().mmb_debug_pchol(device, n, d, dptr(P), dptr(Lp), pos.ctypes.data_as(i32), info.ctypes.data_as(i32)))
+    L = np.zeros((n, d, d))
+    piv = np.zeros((n, d), dtype=np.int32)
+    for c in range(n):
+        if info[c, 0] != d:
+            continue
+        for e in range(d):
+            t = pos[c, e]
+            L[c, e, :t + 1] = Lp[c, tri(t):tri(t) + t + 1]
+            piv[c, t] = e
+    return info[:, 0].copy(), info[:, 1].copy(), L, piv
 
 
 def dptr(a):

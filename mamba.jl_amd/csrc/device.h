@@ -74,7 +74,8 @@ __device__ __forceinline__ void mmb_sqrt_rcp_inrange(double x, double* s, double
   *rcp = mmb_rcp_inrange(*s);
 }
 
-// AMM factorization counters per chain (mmb_amm_stats fields, padded to 32 bytes)
+// AMM factorization counters per chain (mmb_amm_stats fields; 64-bit: a chain adds up to d = 30 to
+// the rank and step sums per update, which would wrap 32 bits after ~1.4e8 updates; padded to 64 bytes)
 #define MMB_AMM_STAT_STRIDE 8
 
 // Per-block descriptor passed in kernel arguments (constant memory, uniform access).
@@ -98,7 +99,7 @@ struct DBlock {
   double* t_xnext;       // AMM   [K][DP] next iteration's proposal minus v (samplers.h amm: formed
                          //       with the factor still in registers), valid when t_xtag[c] matches
   int64_t* t_xtag;       // AMM   [K] (xepoch << 32) | iteration the carried proposal is for
-  uint32_t* t_astat;     // AMM   [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats), diagnostics
+  uint64_t* t_astat;     // AMM   [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats), diagnostics
   double* t_nuts;        // NUTS  [K][8] eps, epsbar, Hbar, mu, alpha, nalpha, -, -
   double* t_nfr;         // NUTS  [K][NutsFrames<DV>::DBL] tree frames (scratch, nuts.h)
   double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)
@@ -139,10 +140,23 @@ struct SweepArgs {
   int32_t ir_vs;         // doubles per chain row of `vals` (P rounded up to 32)
   int32_t ir_amm;        // AMM scratch doubles at the start of a chain's LDS (0 without AMM)
   int32_t ir_lds;        // LDS doubles per chain
-  const int32_t* cperm;  // lane-group slot -> chain (null: identity), engine.cpp order_chains
-  int32_t amwg_exact;    // MMB_AMWG_EXACT: 1 = AMWG and Slice take their sequential paths (samplers.h
-                         // amwg, slice_uni / slice_multi), 2 = AMWG certainty band widened 2^30
-                         // times (tests: frequent fallback)
+  const int32_t* cperm;  // lane-group slot -> chain (null: identity), sweep.hip order_chains_kernel
+  int32_t amwg_exact;    // MMB_AMWG_EXACT: 1 = AMWG takes amwg_sub!'s sequential loop (samplers.h amwg),
+                         // 2 = AMWG certainty band widened 2^30 times (tests: frequent fallback)
+  int32_t slice_exact;   // MMB_SLICE_EXACT=1: Slice evaluates one shrink candidate at a time (slice_uni /
+                         // slice_multi) instead of four per round
+  int32_t amwg_probe;    // MMB_AMWG_PROBE=1 (tests only): near-threshold AMWG accept uniforms
+                         // (mmb_math.h mmb_amwg_probe_factor)
+};
+
+// Wavefront pairing (sweep.hip order_chains_kernel): classes from the first MMB_ORDER_BLOCKS AMM
+// blocks' factor-valid flags
+#define MMB_ORDER_BLOCKS 3
+struct OrderArgs {
+  const int32_t* flags[MMB_ORDER_BLOCKS];  // AMM blocks' t_flags, [K] each
+  int32_t nblk;
+  int32_t K;
+  int32_t* perm;                           // out: slot -> chain
 };
 
 // Block descriptors are read-only for a launch: read them through the constant address

@@ -26,6 +26,9 @@
 #include <rccl/rccl.h>
 
 hipError_t mmb_launch_sweep(int model, unsigned kinds, const SweepArgs& A, hipStream_t st);
+hipError_t mmb_launch_order_chains(const OrderArgs& a, hipStream_t st);
+hipError_t mmb_launch_pchol_probe(int n, int d, const double* S, double* L, int32_t* pos, int32_t* info,
+                                  hipStream_t st);
 hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound, int fold, hipStream_t st);
 hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, int fold, hipStream_t st);
 hipError_t mmb_launch_gr_range(int pmon, int64_t n, int K, const double* draws, double* out,
@@ -53,7 +56,7 @@ struct BlockHost {
   uint8_t* piv = nullptr;
   double* xnext = nullptr;   // AMM carried next proposal [K][DP] (samplers.h amm)
   int64_t* xtag = nullptr;   // AMM [K] tag of the carried proposal
-  uint32_t* astat = nullptr; // AMM [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats)
+  uint64_t* astat = nullptr; // AMM [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats)
 };
 
 struct mmb_engine {
@@ -946,7 +949,7 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
       HIPCHK(e, dalloc(&h.xtag, K));
       HIPCHK(e, hipMemset(h.xtag, 0xff, K * sizeof(int64_t)));  // -1: no carried proposal
       HIPCHK(e, dalloc(&h.astat, K * MMB_AMM_STAT_STRIDE));
-      HIPCHK(e, hipMemset(h.astat, 0, K * MMB_AMM_STAT_STRIDE * sizeof(uint32_t)));
+      HIPCHK(e, hipMemset(h.astat, 0, K * MMB_AMM_STAT_STRIDE * sizeof(uint64_t)));
       HIPCHK(e, dalloc(&h.sigl_d, (size_t)h.d * h.d));
       HIPCHK(e, hipMemcpy(h.sigl_d, h.sigl.data(), h.sigl.size() * sizeof(double), hipMemcpyHostToDevice));
     } else if (h.spec.sampler == MMB_SAMPLER_NUTS) {
@@ -1012,10 +1015,15 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
   A.ig_c = 0.001 * std::log(0.001) - std::lgamma(0.001);
   A.blocks = e->d_blocks;
   A.cperm = e->cperm_identity ? nullptr : e->d_cperm;
-  {  // MMB_AMWG_EXACT=1: AMWG and Slice updates by their sequential loops; 2: wide AMWG band
+  {  // MMB_AMWG_EXACT=1: AMWG updates by amwg_sub!'s sequential loop; 2: wide AMWG band.
+     // MMB_SLICE_EXACT=1: Slice shrink candidates one at a time.  MMB_AMWG_PROBE=1: tests only.
     const char* ae = std::getenv("MMB_AMWG_EXACT");
     const int v = ae ? std::atoi(ae) : 0;
     A.amwg_exact = (v == 1 || v == 2) ? v : 0;
+    const char* se = std::getenv("MMB_SLICE_EXACT");
+    A.slice_exact = (se && std::atoi(se) == 1) ? 1 : 0;
+    const char* ap = std::getenv("MMB_AMWG_PROBE");
+    A.amwg_probe = (ap && std::atoi(ap) == 1) ? 1 : 0;
   }
   if (e->model == MMB_MODEL_IR) {
     A.ir_nodes = e->d_ir_nodes; A.ir_code = e->d_ir_code; A.ir_const = e->d_ir_const;
@@ -1064,46 +1072,36 @@ static int h2d(mmb_engine* e, T* d, const std::vector<T>& h) {
 // chains by class -- for each AMM block, whether the chain has a valid factor (flags bit 2) --
 // so chains that stop alike share wavefronts; the kernel maps lane-group slot -> chain through
 // the table (sweep.h), and every chain keeps its own state, draws column and Philox id, so the
-// results are identical for any order.  MMB_ORDER_CHAINS=0 keeps the identity.
+// results are identical for any order.  The table is a stable counting sort computed on the
+// device (sweep.hip order_chains_kernel), queued on the engine stream behind the previous
+// window: no synchronisation, no copy and no host work per call.  MMB_ORDER_CHAINS=0 keeps the
+// identity.
 static int order_chains(mmb_engine* e) {
+  e->cperm_identity = true;
   if (!(e->model == MMB_MODEL_RATS || e->model == MMB_MODEL_IR) || e->K < 4) return 0;
-  std::vector<const BlockHost*> amm;
-  for (const BlockHost& h : e->blocks)
-    if (h.spec.sampler == MMB_SAMPLER_AMM && h.flags) amm.push_back(&h);
   const char* env = std::getenv("MMB_ORDER_CHAINS");
-  const bool off = env && std::string(env) == "0";
-  if (amm.empty() || off) {
-    e->cperm_identity = true;
-    return 0;
-  }
-  const int64_t K = e->K;
-  // key: per AMM block (first block most significant), whether the chain has a valid factor;
-  // the sort is stable, so chains of a class stay in index order (neighbouring slots keep
-  // neighbouring state rows: adding the mean rank to the key, which scatters them, measured 8 %
-  // slower although it pairs the stopping steps more closely)
-  std::vector<uint32_t> cls((size_t)K, 0u);
-  std::vector<int32_t> fl;
-  for (size_t a = 0; a < amm.size() && a < 16; ++a) {
-    int rc = d2h(e, fl, amm[a]->flags, (size_t)K);
-    if (rc) return rc;
-    for (int64_t k = 0; k < K; ++k) cls[k] = (cls[k] << 1) | (uint32_t)((fl[k] >> 2) & 1);
-  }
-  std::vector<int32_t> perm((size_t)K);
-  std::vector<std::pair<uint32_t, int32_t>> key((size_t)K);
-  for (int64_t k = 0; k < K; ++k) key[k] = {cls[k], (int32_t)k};
-  std::stable_sort(key.begin(), key.end(),
-                   [](const std::pair<uint32_t, int32_t>& x, const std::pair<uint32_t, int32_t>& y) {
-                     return x.first < y.first;
-                   });
-  bool ident = true;
-  for (int64_t k = 0; k < K; ++k) {
-    perm[k] = key[k].second;
-    ident = ident && perm[k] == (int32_t)k;
-  }
-  e->cperm_identity = ident;
-  if (ident) return 0;
-  if (!e->d_cperm) HIPCHK(e, dalloc(&e->d_cperm, (size_t)K));
-  return h2d(e, e->d_cperm, perm);
+  if (env && std::string(env) == "0") return 0;
+  OrderArgs oa;
+  std::memset(&oa, 0, sizeof oa);
+  for (const BlockHost& h : e->blocks)
+    if (h.spec.sampler == MMB_SAMPLER_AMM && h.flags && oa.nblk < MMB_ORDER_BLOCKS) oa.flags[oa.nblk++] = h.flags;
+  if (oa.nblk == 0) return 0;
+  if (!e->d_cperm) HIPCHK(e, dalloc(&e->d_cperm, (size_t)e->K));
+  oa.K = (int32_t)e->K;
+  oa.perm = e->d_cperm;
+  hipError_t st = mmb_launch_order_chains(oa, e->stream);
+  if (st != hipSuccess) return fail(e, MMB_E_HIP, "order_chains launch: %s", hipGetErrorString(st));
+  e->cperm_identity = false;
+  return 0;
+}
+
+// Launch widths of a window: ceil(iters / W) launches of equal length (+-1), so a window of 20
+// iterations at W = 16 runs 10 + 10 instead of 16 + 4 (a short launch pays the launch tail on
+// few iterations)
+static int launch_width(int64_t iters, int W, int64_t li) {
+  const int64_t nl = (iters + W - 1) / W;
+  const int64_t q = iters / nl, r = iters % nl;
+  return (int)(q + (li < r ? 1 : 0));
 }
 
 
@@ -1248,7 +1246,6 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
   }
   if (e->model == MMB_MODEL_LOGISTIC) return run_logistic(e, a, (want && nk > 0) ? e->d_draws : nullptr, kept0, nk, want);
   if (a->iters > 0) {
-    HIPCHK(e, hipStreamSynchronize(e->stream));  // the flags of the previous window
     int orc = order_chains(e);
     if (orc) return orc;
   }
@@ -1271,8 +1268,8 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
       e->evpool.push_back(ev);
     }
   }
-  for (int64_t done = 0, li = 0; done < a->iters; done += W, ++li) {
-    int w = (int)std::min<int64_t>(W, a->iters - done);
+  for (int64_t done = 0, li = 0, w = 0; done < a->iters; done += w, ++li) {
+    w = launch_width(a->iters, W, li);
     A.iter0 = it0 + done;
     A.n_iters = w;
     if (a->time_kernels) HIPCHK(e, hipEventRecord(e->evpool[2 * li], e->stream));
@@ -1711,14 +1708,51 @@ int mmb_amm_stats(mmb_engine* e, int64_t* out) {
   if (e->K == 0) return 0;
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  std::vector<uint32_t> h;
+  std::vector<uint64_t> h;
   for (size_t b = 0; b < e->blocks.size(); ++b) {
     if (!e->blocks[b].astat) continue;
     int rc = d2h(e, h, e->blocks[b].astat, (size_t)e->K * MMB_AMM_STAT_STRIDE);
     if (rc) return rc;
     for (int64_t k = 0; k < e->K; ++k)
-      for (int i = 0; i < MMB_AMM_STATS; ++i) out[b * MMB_AMM_STATS + i] += h[k * MMB_AMM_STAT_STRIDE + i];
+      for (int i = 0; i < MMB_AMM_STATS; ++i) out[b * MMB_AMM_STATS + i] += (int64_t)h[k * MMB_AMM_STAT_STRIDE + i];
   }
+  return 0;
+}
+
+int mmb_chain_order(mmb_engine* e, int32_t* slot_to_chain) {
+  if (!e || !slot_to_chain) return fail(e, MMB_E_ARG, "null argument");
+  if (e->K == 0) return 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (e->cperm_identity || !e->d_cperm) {
+    for (int64_t k = 0; k < e->K; ++k) slot_to_chain[k] = (int32_t)k;
+    return 0;
+  }
+  HIPCHK(e, hipMemcpy(slot_to_chain, e->d_cperm, (size_t)e->K * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int mmb_debug_pchol(int device, int64_t n, int d, const double* S, double* L, int32_t* pos, int32_t* info) {
+  if (n < 1 || d < 1 || d > 30 || !S || !L || !pos || !info)
+    return fail(nullptr, MMB_E_ARG, "mmb_debug_pchol: n >= 1, 1 <= d <= 30 and non-null buffers required");
+  constexpr int TP = 480;
+  hipError_t st = hipSetDevice(device);
+  double *dS = nullptr, *dL = nullptr;
+  int32_t *dpos = nullptr, *dinfo = nullptr;
+  if (st == hipSuccess) st = hipMalloc(&dS, (size_t)n * TP * sizeof(double));
+  if (st == hipSuccess) st = hipMalloc(&dL, (size_t)n * TP * sizeof(double));
+  if (st == hipSuccess) st = hipMalloc(&dpos, (size_t)n * 32 * sizeof(int32_t));
+  if (st == hipSuccess) st = hipMalloc(&dinfo, (size_t)n * 2 * sizeof(int32_t));
+  if (st == hipSuccess) st = hipMemcpy(dS, S, (size_t)n * TP * sizeof(double), hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemset(dL, 0, (size_t)n * TP * sizeof(double));
+  if (st == hipSuccess) st = mmb_launch_pchol_probe((int)n, d, dS, dL, dpos, dinfo, nullptr);
+  if (st == hipSuccess) st = hipDeviceSynchronize();
+  if (st == hipSuccess) st = hipMemcpy(L, dL, (size_t)n * TP * sizeof(double), hipMemcpyDeviceToHost);
+  if (st == hipSuccess) st = hipMemcpy(pos, dpos, (size_t)n * 32 * sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (st == hipSuccess) st = hipMemcpy(info, dinfo, (size_t)n * 2 * sizeof(int32_t), hipMemcpyDeviceToHost);
+  for (void* p : {(void*)dS, (void*)dL, (void*)dpos, (void*)dinfo})
+    if (p) (void)hipFree(p);
+  if (st != hipSuccess) return fail(nullptr, MMB_E_HIP, "mmb_debug_pchol: %s", hipGetErrorString(st));
   return 0;
 }
 

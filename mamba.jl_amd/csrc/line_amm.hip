@@ -510,7 +510,7 @@ __global__ __launch_bounds__(64) void line_amm_kernel(const SweepArgs A) {
   if (lane == 0) {
     ML::store(A, c, 0, s);
     if (B.t_astat != nullptr && st_fac != 0u) {
-      uint32_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
+      uint64_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
       a[0] += st_fac;
       a[1] += st_full;
       a[2] += st_rank;

@@ -108,6 +108,35 @@ MMB_HD double mmb_uniform(const mmb_rng* s, uint32_t k) {
   return mmb_u01((k & 1u) ? b : a);
 }
 
+/* Test-only AMWG probe (MMB_AMWG_PROBE=1, kernels and oracle alike): coordinate j's accept
+ * uniform becomes exp(d_j) * (1 + k 2^-52), d_j the coordinate's log-density difference formed
+ * from its own terms (samplers.h amwg_lanes), so the uniforms sit a few ulps to ~2^-12 off the
+ * accept threshold.  Per block update (the uniform stream's chain, iteration and tag) a hash
+ * picks mode 0 -- every |k| >= 2^20, outside the lane-parallel decision's band, so the update
+ * is decided lane-parallel -- or mode 1 -- |k| in {0, 2^3 .. 2^18}, the band edge and inside, so
+ * the update falls back to the sequential loop; the sign is per coordinate.  This returns
+ * 1 + k 2^-52 (exact). */
+MMB_HD double mmb_amwg_probe_factor(const mmb_rng* s, uint32_t j) {
+  uint32_t h = (s->chain * 0x9E3779B1u) ^ (s->iter * 0x85EBCA77u) ^ (s->tag * 0xC2B2AE3Du);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  uint32_t q = h ^ (j * 0x27D4EB2Fu);
+  q ^= q >> 13;
+  q *= 0x165667B1u;
+  q ^= q >> 16;
+  int e;
+  if ((h & 1u) == 0u) {
+    const uint32_t r = q & 3u;
+    e = r == 0u ? 20 : r == 1u ? 24 : r == 2u ? 30 : 40;
+  } else {
+    e = 3 + (int)(q & 15u);  /* 3 .. 18 */
+    if (((q >> 4) & 7u) == 0u) return 1.0;  /* k = 0 */
+  }
+  const double f = mmb_u2d((uint64_t)(1023 + e - 52) << 52); /* 2^(e - 52) */
+  return ((q >> 8) & 1u) ? 1.0 - f : 1.0 + f;
+}
+
 /* ------------------------------------------------------------------ log (fdlibm e_log.c) */
 MMB_HD double mmb_log(double x) {
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
@@ -212,6 +241,15 @@ MMB_HD double mmb_exp(double x) {
 }
 
 /* log1p via the Goldberg trick (exact-argument correction) */
+/* The probe's uniform (see mmb_amwg_probe_factor): exp(d_j) (1 + k 2^-52), kept inside a uniform's
+ * range [0, 1) -- the lane-parallel decision's certainty tests assume it (a threshold >= 1 is a
+ * certain accept for every real uniform); a NaN d_j gives the largest uniform. */
+MMB_HD double mmb_amwg_probe_uniform(double del, const mmb_rng* s, uint32_t j) {
+  const double u = mmb_exp(del) * mmb_amwg_probe_factor(s, j);
+  const double umax = 0x1.fffffffffffffp-1;
+  return u < umax ? u : umax;
+}
+
 MMB_HD double mmb_log1p(double t) {
   double u = 1.0 + t;
   if (u == 1.0) return t;

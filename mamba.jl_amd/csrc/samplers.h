@@ -154,6 +154,16 @@ struct Smp {
     }
     bool seq = true;
     if constexpr (M::AMWG_SEP && G == 32 && R == 1) {
+      if (A.amwg_probe != 0 && M::amwg_sep(B)) {
+        // test-only (MMB_AMWG_PROBE=1): uniforms a few ulps to 2^-12 off each coordinate's accept
+        // threshold exp(d_j) (mmb_math.h mmb_amwg_probe_factor; the oracle draws the same), so
+        // both the lane-parallel decision and its sequential fallback meet near-ties
+        double tp0, ts0, tp1, ts1;
+        M::amwg_terms(A, pc, s, l, g.lane, x[0], tp0, ts0);
+        M::amwg_terms(A, pc, s, l, g.lane, x[0] + z[0], tp1, ts1);
+        const double del = (tp1 - tp0) + (-0.5 * M::amwg_invv(pc)) * (ts1 - ts0);
+        uown[0] = g.lane < d ? mmb_amwg_probe_uniform(del, &ru, (uint32_t)g.lane) : 0.0;
+      }
       if (A.amwg_exact != 1 && M::amwg_sep(B)) {
         seq = !amwg_lanes(B, pc, s, l, g, x, z, uown, acc, ad, A);
         if (seq && g.lane == 0) atomicAdd(&A.nuts_stat[5], 1ull);
@@ -1058,12 +1068,12 @@ struct Smp {
     if (g.lane == 0) {
       // no-return atomics: fire-and-forget, no HBM round trip on the update's path (a plain
       // load-add-store would wait for the load)
-      uint32_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
-      (void)__hip_atomic_fetch_add(a + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (rank == d) (void)__hip_atomic_fetch_add(a + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      (void)__hip_atomic_fetch_add(a + 2, (uint32_t)rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      (void)__hip_atomic_fetch_add(a + 3, (uint32_t)ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (redo) (void)__hip_atomic_fetch_add(a + 4, (uint32_t)redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t* a = B.t_astat + (size_t)c * MMB_AMM_STAT_STRIDE;
+      (void)__hip_atomic_fetch_add(a + 0, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (rank == d) (void)__hip_atomic_fetch_add(a + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      (void)__hip_atomic_fetch_add(a + 2, (uint64_t)rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      (void)__hip_atomic_fetch_add(a + 3, (uint64_t)ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (redo) (void)__hip_atomic_fetch_add(a + 4, (uint64_t)redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
@@ -1495,7 +1505,7 @@ struct Smp {
   __device__ __forceinline__ static void slice_uni(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
                                    const Lc& l, const Grp<G>& g, double* lds) {
     if constexpr (M::SLICE_CAND && G == 32 && R == 1) {
-      if (A.amwg_exact != 1 && M::slice_cand_ok(B)) {
+      if (A.slice_exact == 0 && M::slice_cand_ok(B)) {
         slice_uni_cand(A, B, ru, s, l, g, lds);
         return;
       }
@@ -1642,7 +1652,7 @@ struct Smp {
   __device__ __forceinline__ static void slice_multi(const SweepArgs& A, const DBlock& B, const mmb_rng& ru, St& s,
                                      const Lc& l, const Grp<G>& g, double* lds) {
     if constexpr (M::SLICE_CAND && G == 32 && R == 1) {
-      if (A.amwg_exact != 1 && M::slice_cand_ok(B)) {
+      if (A.slice_exact == 0 && M::slice_cand_ok(B)) {
         slice_multi_cand(A, B, ru, s, l, g, lds);
         return;
       }

@@ -26,6 +26,64 @@ static hipError_t launch(const SweepArgs& A, hipStream_t st, int threads) {
   return hipGetLastError();
 }
 
+// Wavefront pairing (engine.cpp order_chains): the slot -> chain table of the next window as a
+// stable counting sort of the chains by class, on the engine stream right behind the previous
+// window's last launch (no host round trip).  Class of chain k: per AMM block (the first block
+// most significant, at most MMB_ORDER_BLOCKS of them), whether it holds a valid factor (flags
+// bit 2).  One workgroup: thread t owns chains [t*C, (t+1)*C); the per-(class, thread) counts sit
+// in LDS class-major, so one exclusive scan of that array gives every thread the first slot of
+// its chains of each class, and chains of one class keep their index order.
+constexpr int ORD_T = 1024;
+__global__ __launch_bounds__(ORD_T) void order_chains_kernel(const OrderArgs a) {
+  __shared__ int32_t cnt[(1 << MMB_ORDER_BLOCKS) * ORD_T];
+  __shared__ int32_t wsum[ORD_T / 64];
+  const int t = (int)threadIdx.x;
+  const int NC = 1 << a.nblk;
+  const int C = (a.K + ORD_T - 1) / ORD_T;
+  const int k0 = min(a.K, t * C), k1 = min(a.K, k0 + C);
+  auto cls = [&](int k) {
+    int c = 0;
+    for (int b = 0; b < a.nblk; ++b) c = (c << 1) | ((a.flags[b][k] >> 2) & 1);
+    return c;
+  };
+  for (int c = 0; c < NC; ++c) cnt[c * ORD_T + t] = 0;
+  for (int k = k0; k < k1; ++k) cnt[cls(k) * ORD_T + t] += 1;
+  __syncthreads();
+  // exclusive scan of cnt[0 .. NC*T): thread t owns NC consecutive entries
+  int* own = cnt + t * NC;
+  int s = 0;
+  for (int i = 0; i < NC; ++i) s += own[i];
+  const int lane = t & 63, w = t >> 6;
+  int inc = s;  // inclusive wave scan
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  int run = base + inc - s;
+  __syncthreads();  // every thread has read the counts it owns before they are overwritten
+  for (int i = 0; i < NC; ++i) {
+    const int v = own[i];
+    own[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int k = k0; k < k1; ++k) {
+    int* p = &cnt[cls(k) * ORD_T + t];
+    a.perm[*p] = k;
+    *p += 1;
+  }
+}
+
+hipError_t mmb_launch_order_chains(const OrderArgs& a, hipStream_t st) {
+  if (a.nblk < 1 || a.nblk > MMB_ORDER_BLOCKS || a.K < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(order_chains_kernel, dim3(1), dim3(ORD_T), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t mmb_launch_line_amm(const SweepArgs& A, hipStream_t st);  // line_amm.hip
 
 // host-side launcher (engine.cpp); kinds = bitmask of the scheme's sampler kinds

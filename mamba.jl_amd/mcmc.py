@@ -164,6 +164,14 @@ class Engine:
         self._chk(self.lib.mmb_amwg_stats(self.h, v))
         return {"sequential_updates": v[0]}
 
+    def chain_order(self):
+        """The lane-group slot -> chain table of the last window (mmb_chain_order): the 32-lane
+        kernels pair chains whose AMM factorization stops alike; results do not depend on it."""
+        out = np.empty(self.K, dtype=np.int32)
+        if self.K:
+            self._chk(self.lib.mmb_chain_order(self.h, out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out
+
     def ir_jit(self):
         """Node-IR engines: (True, info) when the specialised kernel runs (mmb_create_ir compiled
         the model with hipRTC or found it in the cache), (False, reason) for the interpreter."""

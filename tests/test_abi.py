@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(mamba):
     assert len(syms) >= 20
     missing = [s for s in syms if s not in exported]
     assert not missing, missing
-    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 8
+    assert lib.mmb_abi_version() == mamba.abi.MMB_ABI_VERSION == 9
 
 
 def test_struct_layout_matches_header(mamba):

@@ -136,9 +136,11 @@ def test_amm_stats_match_oracle(mamba, oracle, case, monkeypatch):
 
 def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
     """engine.cpp order_chains pairs chains of one factor-validity class in a wavefront before
-    every window (the second window below runs permuted: the first set the flags).  Every chain
-    keeps its own state, draws column and Philox id, so the draws, values and tune equal the
-    identity-order run (MMB_ORDER_CHAINS=0) and the oracle bit for bit."""
+    every window (the second window below runs permuted: the first set the flags).  The table is
+    computed on the device (sweep.hip order_chains_kernel) and must be the stable sort of the
+    chains by (alpha valid, beta valid) at the window start.  Every chain keeps its own state,
+    draws column and Philox id, so the draws, values and tune equal the identity-order run
+    (MMB_ORDER_CHAINS=0) and the oracle bit for bit."""
     m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
     init = mamba.model.rats_init_ls(16384, seed=1000)[:600]
     out = {}
@@ -148,8 +150,16 @@ def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
         eng = mamba.Engine(m)
         eng.init_chains(init, seed=33)
         a = eng.run(90, burnin=0, thin=3)
+        ta = eng.tune()
         b = eng.run(60, burnin=0, thin=3)
         out[mode] = (a, b, eng.values(), eng.tune())
+        order = eng.chain_order()
+        if mode == "identity":
+            np.testing.assert_array_equal(order, np.arange(init.shape[0]))
+        else:
+            (oa, da), (ob, db) = [(o, d) for o, d in _amm_offsets(mamba, m)]
+            key = (ta[:, oa + 2] != 0).astype(int) * 2 + (ta[:, ob + 2] != 0).astype(int)
+            np.testing.assert_array_equal(order, np.argsort(key, kind="stable"))
     for x, y in zip(out["ordered"], out["identity"]):
         np.testing.assert_array_equal(x, y)
     st = oracle.new_state(m, init)
@@ -159,12 +169,22 @@ def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
     assert 0.2 < (tv[:, 2] != 0).mean() < 0.9  # alpha factor validity split: the order is not the identity
 
 
+def _amm_offsets(mamba, m):
+    """(offset in the canonical tune row, d) of each AMM block."""
+    out, off = [], 0
+    for s, n in zip(m.samplers, mamba_tune_lens(mamba, m)):
+        if s.kind == mamba.abi.MMB_SAMPLER_AMM:
+            out.append((off, m.block_dim(s)))
+        off += n
+    return out
+
+
 def test_amwg_lane_parallel_path_matches_sequential(mamba, oracle, monkeypatch):
     """samplers.h amwg_lanes decides every coordinate of the rats alpha / beta AMWG blocks at
     once when each accept test is certain under the logpdf's rounding bound, and falls back to
     amwg_sub!'s sequential loop otherwise; the scalar-block Slice updates evaluate their shrink
     candidates four at a time (slice_uni_cand / slice_multi_cand).  Default, sequential-only
-    for both (MMB_AMWG_EXACT=1) and a
+    for both (MMB_AMWG_EXACT=1 with MMB_SLICE_EXACT=1) and a
     2^30 times wider band (=2: many chains of a wavefront fall back while their partner does
     not) give the same draws, values and tune as the oracle, bit for bit; by default the
     fallback is rare."""
@@ -174,6 +194,7 @@ def test_amwg_lane_parallel_path_matches_sequential(mamba, oracle, monkeypatch):
     out, seqn = {}, {}
     for mode in ("0", "1", "2"):
         monkeypatch.setenv("MMB_AMWG_EXACT", mode)
+        monkeypatch.setenv("MMB_SLICE_EXACT", "1" if mode == "1" else "0")
         eng = mamba.Engine(m)
         eng.init_chains(init, seed=71)
         d = eng.run(iters, burnin=30, thin=2)

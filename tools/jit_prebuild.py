@@ -2,7 +2,7 @@
 tests and bench.py create, into the in-tree cache (mamba.jl_amd/lib/jit, next to the library),
 on the CPU -- a build step like the library itself, so no GPU run pays a compile.
 
-  python tools/jit_prebuild.py [-j 8]
+  python tools/jit_prebuild.py [-j 3]
 
 The cache key is a hash of the generated source (the model's structure, not its data), the
 embedded headers, the options and the hipRTC version.
@@ -59,7 +59,7 @@ def build_one(i):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("-j", type=int, default=8)
+    ap.add_argument("-j", type=int, default=3)  # hipRTC compiles take several GB each
     a = ap.parse_args()
     n = len(models())
     import multiprocessing as mp
