@@ -71,6 +71,9 @@ def parse():
                    help="logistic: Model.burnin of the timed run (default steps // 2: 1000 of 2000)")
     p.add_argument("--scheme", default="gibbs_amm",
                    help="gibbs_amm (metric config) | reference | ablations: amm_noadapt, gibbs_only")
+    p.add_argument("--amm-fullrank", action="store_true",
+                   help="ablation (rats gibbs_amm): AMM moments seeded positive definite, so every "
+                        "factorization reaches full rank (no amm.jl:102 alias chains)")
     a = p.parse_args()
     # logistic (configs[3]): the timed steps are the config's whole run, 2000
     # iterations with NUTS adapting for the first 1000 (--nuts-burnin), on re-initialised chains
@@ -248,6 +251,34 @@ def amm_window(model, before, after):
     return out
 
 
+def seed_fullrank_moments(mb, model, eng):
+    """Ablation: every AMM block's moments start as if from m = 1000 draws with covariance D
+    (alpha 6.0, beta 0.05: about the posterior variances), Mv = the current block value, no
+    alias (amm.jl:102) and no factor yet.  Sigma = Mvv - Mv Mv' = D stays positive definite under
+    the running averages, so every timed factorization runs all n pivots: the intrinsic cost of
+    the update, which the headline's alias-stopped chains (about half) do not pay."""
+    import numpy as np
+    t, v = eng.tune(), eng.values()
+    off, T = 0, lambda i: i * (i + 1) // 2  # noqa: E731
+    vo = {"alpha": 1, "beta": 33}
+    var = {"alpha": 6.0, "beta": 0.05}
+    for s in model.samplers:
+        d = model.block_dim(s)
+        if s.kind == mb.abi.MMB_SAMPLER_AMM:
+            name = s.params if isinstance(s.params, str) else s.params[0]
+            x = v[:, vo[name]:vo[name] + d]
+            r = t[:, off:off + 4 + 2 * d + 2 * T(d)]
+            r[:, 0], r[:, 1], r[:, 2], r[:, 3] = 1.0, 1000.0, 0.0, 0.0
+            r[:, 4:4 + d] = x
+            for i in range(d):
+                r[:, 4 + d + T(i):4 + d + T(i) + i + 1] = x[:, i:i + 1] * x[:, :i + 1]
+                r[:, 4 + d + T(i) + i] += var[name]
+            off += 4 + 2 * d + d * (d + 1)
+        elif s.kind == mb.abi.MMB_SAMPLER_AMWG:
+            off += 2 + 2 * d
+    eng.set_tune(t)
+
+
 def pmc_traffic(args, W):
     """HBM bytes per sweep launch from the committed rocprofv3 PMC pass of this exact kernel
     build and configuration (profiles/, gathered by tools/profiles_run.sh and corrected by
@@ -297,6 +328,10 @@ def main():
     nuts = args.workload == "logistic"
     eng = mb.Engine(model, device=local)
     eng.init_chains(init_all, chain_offset=rank * K, seed=20261015)
+    if args.amm_fullrank:
+        if args.workload != "rats" or args.scheme != "gibbs_amm":
+            raise SystemExit("--amm-fullrank applies to --workload rats --scheme gibbs_amm")
+        seed_fullrank_moments(mb, model, eng)
 
     def barrier():
         if world > 1:
@@ -494,6 +529,9 @@ def main():
                               "scheme": args.scheme})
         if args.scheme == "gibbs_amm":
             out["config"]["amm_adapt"] = "all"
+        if args.amm_fullrank:
+            out["metric"] = "chain-updates/sec, rats Gibbs+AMM full-rank ablation (not the headline)"
+            out["config"]["amm_moments"] = "seeded positive definite (--amm-fullrank): every factorization full rank"
     if amm_timed:
         out["config"]["amm"] = amm_timed
     if n_amwg:

@@ -372,11 +372,13 @@ int mmb_amm_stats(mmb_engine* e, int64_t* out /* MMB_MAX_BLOCKS x MMB_AMM_STATS 
  * Both paths give the same draws; diagnostics only. */
 int mmb_amwg_stats(mmb_engine* e, int64_t* out /* 1 */);
 
-/* The lane-group slot -> chain table the last window ran with (K entries; the identity when
- * no ordering applies).  The 32-lane sweep kernels (rats, node IR) pair chains whose pivoted
- * Cholesky stops alike in one wavefront; the table is a stable sort of the chains by their
- * AMM blocks' factor-valid flags, computed on the device before each window.  Results do not
- * depend on it (every chain keeps its own state, draws column and Philox id); diagnostics. */
+/* The lane-group slot -> chain table the next window will run with (K entries; the identity
+ * when no ordering applies).  The 32-lane sweep kernels (rats, node IR) pair chains whose
+ * pivoted Cholesky stops alike in one wavefront; the table sorts the chains by their AMM blocks'
+ * factor-valid flags (slow classes first; MMB_ORDER_MODE 0 ascending, 2 balanced workgroups),
+ * computed on the device right after each window (and before one that follows a host write of
+ * the tune state).  Results do not depend on it (every chain keeps its own state, draws column
+ * and Philox id); diagnostics. */
 int mmb_chain_order(mmb_engine* e, int32_t* slot_to_chain);
 
 /* Diagnostics: the device's 32-lane pivoted Cholesky of the AMM update (cholfact(Hermitian(S),

@@ -156,6 +156,8 @@ struct OrderArgs {
   const int32_t* flags[MMB_ORDER_BLOCKS];  // AMM blocks' t_flags, [K] each
   int32_t nblk;
   int32_t K;
+  int32_t cpw;                             // chains per workgroup of the sweep kernel
+  int32_t mode;                            // 0 ascending class order, 1 descending, 2 balanced workgroups
   int32_t* perm;                           // out: slot -> chain
 };
 

@@ -89,6 +89,7 @@ struct mmb_engine {
   unsigned long long* lg_ngrad = nullptr;
   int32_t* d_cperm = nullptr;  // lane-group slot -> chain of the 32-lane sweep kernels (order_chains)
   bool cperm_identity = true;
+  bool order_fresh = false;    // d_cperm was computed from the current flags (after the last window)
   unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum}, Slice overflows
                                           // since init_chains
   unsigned long long slice_overflows = 0;  // d_nstat[3] as last reported by mmb_run
@@ -680,6 +681,7 @@ static void free_dev(mmb_engine* e) {
     if (e->d_cperm) (void)hipFree(e->d_cperm);
     e->d_cperm = nullptr;
     e->cperm_identity = true;
+    e->order_fresh = false;
   }
   if (e->d_draws) (void)hipFree(e->d_draws);
   e->d_vals = nullptr;
@@ -1089,6 +1091,16 @@ static int order_chains(mmb_engine* e) {
   if (!e->d_cperm) HIPCHK(e, dalloc(&e->d_cperm, (size_t)e->K));
   oa.K = (int32_t)e->K;
   oa.perm = e->d_cperm;
+  // chains per workgroup of the 32-lane sweep kernels (sweep.hip launch: rats 256 threads, node IR 128)
+  oa.cpw = e->model == MMB_MODEL_RATS ? 8 : 4;
+  {
+    // default 1, slow classes first: the launch's second dispatch round then ends on the fast
+    // ones (20-iteration windows: 1.17-1.18e8 -> 1.20-1.21e8 chain-updates/s; balanced
+    // workgroups, mode 2, 1.12-1.13e8)
+    const char* om = std::getenv("MMB_ORDER_MODE");
+    oa.mode = om ? std::atoi(om) : 1;
+    if (oa.mode < 0 || oa.mode > 2) oa.mode = 1;
+  }
   hipError_t st = mmb_launch_order_chains(oa, e->stream);
   if (st != hipSuccess) return fail(e, MMB_E_HIP, "order_chains launch: %s", hipGetErrorString(st));
   e->cperm_identity = false;
@@ -1245,7 +1257,7 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
     }
   }
   if (e->model == MMB_MODEL_LOGISTIC) return run_logistic(e, a, (want && nk > 0) ? e->d_draws : nullptr, kept0, nk, want);
-  if (a->iters > 0) {
+  if (a->iters > 0 && !e->order_fresh) {  // else computed right after the previous window
     int orc = order_chains(e);
     if (orc) return orc;
   }
@@ -1288,8 +1300,15 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
     e->launches += 1;
     e->units += (int64_t)w * e->K;
   }
+  if (a->iters > 0) {
+    // the next window's order from this window's final flags, queued behind its last launch so
+    // it runs while the host is between windows (a host write of the tune state invalidates it)
+    int orc = order_chains(e);
+    if (orc) return orc;
+    e->order_fresh = true;
+  }
   if (a->time_kernels) {  // per-launch device time, summed after the window (no per-launch sync)
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipEventSynchronize(e->evpool[2 * nl - 1]));
     for (int64_t li = 0; li < nl; ++li) {
       float ms = 0.f;
       HIPCHK(e, hipEventElapsedTime(&ms, e->evpool[2 * li], e->evpool[2 * li + 1]));
@@ -1480,6 +1499,7 @@ int mmb_set_tune(mmb_engine* e, const double* tune) {
     }
   }
   ++e->xepoch;
+  e->order_fresh = false;  // the factor-valid flags change
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   int64_t off = 0;
@@ -1773,6 +1793,9 @@ int mmb_grad_evals(mmb_engine* e, int64_t* n) {
 // its kept draws to the mmb_gr_len sufficient statistics on device (gr.hip), then one SUM
 // all-reduce over RCCL/xGMI, in place in a per-engine device buffer; the global [min, max]
 // used for link() and the shift is one MAX all-reduce of (-min, max).
+// the agreement slot's value outside an agreement: flag 2 = "this rank could not stage" (comm_agree)
+static const double kAgreeFailed[4] = {2.0, 0.0, 0.0, 0.0};
+
 struct mmb_comm {
   std::vector<mmb_engine*> eng;
   std::vector<ncclComm_t> comm;
@@ -1833,7 +1856,10 @@ int mmb_comm_init(mmb_engine** engines, int nlocal, int nranks, int rank0, const
   c->L = mmb_gr_len(e0);
   const size_t nbuf = (size_t)c->L + 4 * (size_t)c->p + 4;
   for (int i = 0; i < nlocal; ++i) {
-    if (hipSetDevice(engines[i]->device) != hipSuccess || hipMalloc(&c->buf[i], nbuf * sizeof(double)) != hipSuccess) {
+    // the agreement slot starts (and is left after every agreement) holding the failure flag, so
+    // a rank that cannot stage its contribution still contributes "failed" (comm_agree)
+    if (hipSetDevice(engines[i]->device) != hipSuccess || hipMalloc(&c->buf[i], nbuf * sizeof(double)) != hipSuccess ||
+        hipMemcpy(c->buf[i] + (nbuf - 4), kAgreeFailed, sizeof kAgreeFailed, hipMemcpyHostToDevice) != hipSuccess) {
       mmb_comm_destroy(c);
       return fail(e0, MMB_E_HIP, "comm buffer allocation failed");
     }
@@ -1885,7 +1911,9 @@ static ncclResult_t grouped_allreduce(mmb_comm* c, size_t off, size_t n, ncclRed
 
 // Agreement step before a data collective.  Every local engine contributes (flag, -n_kept,
 // n_kept) to one MAX all-reduce, where flag = 1 if this process cannot take part (too few kept
-// draws on some local engine).  A process whose precondition fails therefore still enters the
+// draws on some local engine) and 2 if it could not even stage its contribution: the slot holds
+// 2 outside an agreement (set at comm init and re-armed after every readback), so an engine whose
+// staging copy fails contributes the failure flag, never a stale "agree" of an earlier call.  A process whose precondition fails therefore still enters the
 // collective, and every rank sees the same verdict: all fail together (MMB_E_STATE for too few
 // draws, MMB_E_ARG when the ranks kept different numbers of draws, which would otherwise give
 // a silently wrong PSRF) or all proceed with the common n_kept.
@@ -1902,21 +1930,32 @@ static int comm_agree(mmb_comm* c, int64_t need, int64_t* nkept) {
   c->agree[2] = (double)hi;
   c->agree[3] = 0.0;
   int lrc = 0;
+  // MMB_TEST_COMM_STAGE_FAIL=1 (tests only): skip the staging copy as if it had failed
+  const char* tf = std::getenv("MMB_TEST_COMM_STAGE_FAIL");
+  const bool inject = tf && std::atoi(tf) == 1;
   for (size_t i = 0; i < c->eng.size(); ++i) {
     hipError_t st = hipSetDevice(c->eng[i]->device);
+    if (st == hipSuccess && inject) st = hipErrorUnknown;
     if (st == hipSuccess)
       st = hipMemcpyAsync(c->buf[i] + off, c->agree, sizeof(c->agree), hipMemcpyHostToDevice, c->eng[i]->stream);
     if (st != hipSuccess && !lrc) lrc = fail(e0, MMB_E_HIP, "agreement staging: %s", hipGetErrorString(st));
   }
   const ncclResult_t r = grouped_allreduce(c, off, 4, ncclMax);
-  double all[4] = {1.0, 0.0, 0.0, 0.0};
+  double all[4] = {2.0, 0.0, 0.0, 0.0};
   hipError_t st = hipSetDevice(e0->device);
   if (st == hipSuccess) st = hipMemcpyAsync(all, c->buf[0] + off, sizeof(all), hipMemcpyDeviceToHost, e0->stream);
+  for (size_t i = 0; i < c->eng.size(); ++i)  // re-arm: the slot holds the failure flag again
+    if (hipSetDevice(c->eng[i]->device) == hipSuccess)
+      (void)hipMemcpyAsync(c->buf[i] + off, kAgreeFailed, sizeof kAgreeFailed, hipMemcpyHostToDevice, c->eng[i]->stream);
   const int rc = comm_sync(c);
   if (r != ncclSuccess) return fail(e0, MMB_E_COMM, "agreement all-reduce: %s", ncclGetErrorString(r));
-  if (lrc) return lrc;
+  if (lrc)
+    return fail(e0, MMB_E_HIP, "%s (the agreement all-reduce saw flag %.0f: every rank fails this collective)",
+                g_last_error.c_str(), all[0]);
   if (st != hipSuccess) return fail(e0, MMB_E_HIP, "agreement readback: %s", hipGetErrorString(st));
   if (rc) return rc;
+  if (all[0] >= 2.0)
+    return fail(e0, MMB_E_COMM, "another rank could not stage its agreement contribution; collective skipped");
   if (all[0] != 0.0)
     return fail(e0, MMB_E_STATE, "need >= %lld device-kept draws per chain on every rank (this process: %lld)",
                 (long long)need, (long long)lo);

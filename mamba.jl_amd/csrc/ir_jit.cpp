@@ -189,7 +189,12 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
   return o.str();
 }
 
-static const char* const kOpts[] = {"-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off",
+// the target of the specialised kernels is the library's own (build.py passes PYTORCH_ROCM_ARCH as
+// MMB_ARCH), so they run wherever the static kernels do; it is part of the cache key via kOpts
+#ifndef MMB_ARCH
+#define MMB_ARCH "gfx950"
+#endif
+static const char* const kOpts[] = {"-O3", "--offload-arch=" MMB_ARCH, "-std=c++17", "-ffp-contract=off",
                                     "-mllvm", "-pragma-unroll-threshold=100000"};
 
 int mmb_ir_jit_obtain(const std::string& src, std::vector<char>* code, std::string* info) {

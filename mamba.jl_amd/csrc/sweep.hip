@@ -34,18 +34,26 @@ static hipError_t launch(const SweepArgs& A, hipStream_t st, int threads) {
 // in LDS class-major, so one exclusive scan of that array gives every thread the first slot of
 // its chains of each class, and chains of one class keep their index order.
 constexpr int ORD_T = 1024;
+constexpr int ORD_KC = 16384;  // shards up to this size read the flags once, coalesced, into LDS
 __global__ __launch_bounds__(ORD_T) void order_chains_kernel(const OrderArgs a) {
   __shared__ int32_t cnt[(1 << MMB_ORDER_BLOCKS) * ORD_T];
   __shared__ int32_t wsum[ORD_T / 64];
+  __shared__ uint8_t ccls[ORD_KC];
   const int t = (int)threadIdx.x;
   const int NC = 1 << a.nblk;
   const int C = (a.K + ORD_T - 1) / ORD_T;
   const int k0 = min(a.K, t * C), k1 = min(a.K, k0 + C);
-  auto cls = [&](int k) {
+  auto gcls = [&](int k) {
     int c = 0;
     for (int b = 0; b < a.nblk; ++b) c = (c << 1) | ((a.flags[b][k] >> 2) & 1);
     return c;
   };
+  const bool cached = a.K <= ORD_KC;
+  if (cached) {
+    for (int k = t; k < a.K; k += ORD_T) ccls[k] = (uint8_t)gcls(k);
+    __syncthreads();
+  }
+  auto cls = [&](int k) { return cached ? (int)ccls[k] : gcls(k); };
   for (int c = 0; c < NC; ++c) cnt[c * ORD_T + t] = 0;
   for (int k = k0; k < k1; ++k) cnt[cls(k) * ORD_T + t] += 1;
   __syncthreads();
@@ -71,10 +79,21 @@ __global__ __launch_bounds__(ORD_T) void order_chains_kernel(const OrderArgs a) 
     run += v;
   }
   __syncthreads();
+  // sorted position -> slot.  mode 1: reversed (slow classes dispatched first).  mode 2: the chain pairs of a wavefront stay consecutive in the
+  // sorted order, but the W waves of a workgroup take their pairs from W different stretches of
+  // it (pair q -> wave q / NF of workgroup q % NF, NF full workgroups), so every workgroup holds
+  // fast and slow classes alike and the second dispatch round does not end on the slowest ones
+  const int W = a.cpw / 2, NF = a.K / a.cpw;
   for (int k = k0; k < k1; ++k) {
     int* p = &cnt[cls(k) * ORD_T + t];
-    a.perm[*p] = k;
+    int pos = *p;
     *p += 1;
+    if (a.mode == 1) pos = a.K - 1 - pos;
+    if (a.mode == 2 && W > 0 && (pos >> 1) < NF * W) {
+      const int q = pos >> 1;
+      pos = (q % NF) * a.cpw + 2 * (q / NF) + (pos & 1);
+    }
+    a.perm[pos] = k;
   }
 }
 

@@ -137,31 +137,43 @@ def test_amm_stats_match_oracle(mamba, oracle, case, monkeypatch):
 def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
     """engine.cpp order_chains pairs chains of one factor-validity class in a wavefront before
     every window (the second window below runs permuted: the first set the flags).  The table is
-    computed on the device (sweep.hip order_chains_kernel) and must be the stable sort of the
-    chains by (alpha valid, beta valid) at the window start.  Every chain keeps its own state,
+    computed on the device after each window (sweep.hip order_chains_kernel) and must be the
+    sort of the chains by (alpha valid, beta valid) of every MMB_ORDER_MODE.  Every chain keeps its own state,
     draws column and Philox id, so the draws, values and tune equal the identity-order run
     (MMB_ORDER_CHAINS=0) and the oracle bit for bit."""
     m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
     init = mamba.model.rats_init_ls(16384, seed=1000)[:600]
     out = {}
-    for mode in ("ordered", "identity"):
+    for mode in ("ordered", "descending", "balanced", "identity"):
+        monkeypatch.setenv("MMB_ORDER_MODE", {"descending": "1", "balanced": "2"}.get(mode, "0"))
         if mode == "identity":
             monkeypatch.setenv("MMB_ORDER_CHAINS", "0")
         eng = mamba.Engine(m)
         eng.init_chains(init, seed=33)
         a = eng.run(90, burnin=0, thin=3)
-        ta = eng.tune()
         b = eng.run(60, burnin=0, thin=3)
-        out[mode] = (a, b, eng.values(), eng.tune())
-        order = eng.chain_order()
+        ta = eng.tune()
+        out[mode] = (a, b, eng.values(), ta)
+        order = eng.chain_order()  # the next window's table, from the flags after b
+        K = init.shape[0]
         if mode == "identity":
-            np.testing.assert_array_equal(order, np.arange(init.shape[0]))
-        else:
-            (oa, da), (ob, db) = [(o, d) for o, d in _amm_offsets(mamba, m)]
-            key = (ta[:, oa + 2] != 0).astype(int) * 2 + (ta[:, ob + 2] != 0).astype(int)
-            np.testing.assert_array_equal(order, np.argsort(key, kind="stable"))
-    for x, y in zip(out["ordered"], out["identity"]):
-        np.testing.assert_array_equal(x, y)
+            np.testing.assert_array_equal(order, np.arange(K))
+            continue
+        (oa, da), (ob, db) = [(o, d) for o, d in _amm_offsets(mamba, m)]
+        key = (ta[:, oa + 2] != 0).astype(int) * 2 + (ta[:, ob + 2] != 0).astype(int)
+        srt = np.argsort(key, kind="stable")
+        if mode == "descending":
+            srt = srt[::-1]
+        if mode == "balanced":  # pair q -> wave q // NF of workgroup q % NF (8 chains, 4 waves)
+            NF, exp = K // 8, srt.copy()
+            for pos in range(NF * 8):
+                q = pos >> 1
+                exp[(q % NF) * 8 + 2 * (q // NF) + (pos & 1)] = srt[pos]
+            srt = exp
+        np.testing.assert_array_equal(order, srt)
+    for mode in ("ordered", "descending", "balanced"):
+        for x, y in zip(out[mode], out["identity"]):
+            np.testing.assert_array_equal(x, y)
     st = oracle.new_state(m, init)
     do = oracle.run(m, st, 150, burnin=0, thin=3, seed=33, nthreads=8)
     np.testing.assert_array_equal(np.concatenate(out["ordered"][:2]), do)
@@ -699,6 +711,26 @@ def test_gr_allreduce_agreement_fails_together(mamba):
     np.testing.assert_array_equal(comm.gr_allreduce(kinds, shift), eng.gr_partials(kinds, shift))
     comm.close()
     assert d.shape[0] == 20
+
+
+def test_gr_allreduce_stage_failure_reaches_the_collective(mamba, monkeypatch):
+    """A rank whose agreement contribution cannot be staged (injected: MMB_TEST_COMM_STAGE_FAIL)
+    still joins the agreement all-reduce, and what it contributes is the failure flag the slot
+    is armed with -- never the "agree" a previous successful call left there -- so its peers
+    skip the collective instead of waiting in it; the communicator keeps working afterwards."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    eng = mamba.Engine(m)
+    eng.init_chains(mamba.model.rats_init_ls(128, seed=3), seed=4)
+    eng.run(40, burnin=0, thin=2, keep_device=True)
+    comm = mamba.Comm([eng], nranks=1, rank0=0, uid=mamba.Comm.unique_id())
+    kinds, shift = np.array([1, 0, 0], np.int32), np.array([3.6, 6.0, 100.0])
+    ok = comm.gr_allreduce(kinds, shift)                      # leaves a successful agreement behind
+    monkeypatch.setenv("MMB_TEST_COMM_STAGE_FAIL", "1")
+    with pytest.raises(RuntimeError, match=r"error -3 .*agreement staging.*saw flag 2"):
+        comm.gr_allreduce(kinds, shift)
+    monkeypatch.delenv("MMB_TEST_COMM_STAGE_FAIL")
+    np.testing.assert_array_equal(comm.gr_allreduce(kinds, shift), ok)
+    comm.close()
 
 
 def test_rats_scale_total_on_one_gpu(mamba, oracle):
