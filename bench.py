@@ -346,6 +346,11 @@ def main():
     mburn = pre + args.warmup if nuts else 0
     if pre > 0:
         eng.run(pre, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False)
+    early = os.environ.get("MMB_BENCH_STATS_EARLY") == "1"  # (experiment: no host reads after the warm-up)
+    if early and not nuts:
+        eng.reserve_draws(args.steps // thin + 1)
+        amm_before = eng.amm_stats()
+        amwg_before = eng.amwg_stats()["sequential_updates"]
     # warm-up with event timing on (the engine's event pools exist before the timed window),
     # then the device draw buffer for the timed window's kept rows: no allocation in the window
     eng.run(args.warmup, burnin=0, thin=thin, model_burnin=mburn, draws=False, keep_device=False,
@@ -357,10 +362,11 @@ def main():
         # the kernels and the engine's buffers
         eng.init_chains(init_all, chain_offset=rank * K, seed=20261015)
         mburn = tburn = args.nuts_burnin if args.nuts_burnin is not None else args.steps // 2
-    eng.reserve_draws(args.steps // thin + 1)
     nuts_before = eng.nuts_stats() if nuts else None
-    amm_before = eng.amm_stats()
-    amwg_before = eng.amwg_stats()["sequential_updates"]
+    if not (early and not nuts):
+        eng.reserve_draws(args.steps // thin + 1)
+        amm_before = eng.amm_stats()
+        amwg_before = eng.amwg_stats()["sequential_updates"]
     barrier()
     t0 = time.perf_counter()
     eng.run(args.steps, burnin=tburn, thin=thin, model_burnin=mburn, draws=False, keep_device=True,

@@ -105,6 +105,10 @@ struct DBlock {
   double* t_hmc;         // HMC/MALA [K][2] epsilon, L (HMCTune / MALATune, hmc.jl:5-28)
   int32_t ir_blk;        // node IR: index into SweepArgs::ir_blocks
   int32_t fdgrad;        // NUTS/HMC/MALA on line: 1 = Calculus forward differences (mmb_gradient)
+  const int32_t* sep;    // node-IR AMWG block whose logpdf! separates by coordinate (engine.cpp ir_sep_table):
+                         // [d + 2 offsets][entries (term << 24 | element)], entries of coordinate j at
+                         // off[j] .. off[j+1], elements on no coordinate at off[d] .. off[d+1]; null: none
+  double sep_eps;        // its lane-parallel decision's relative rounding band (ir.h amwg_dm)
 };
 
 struct SweepArgs {

@@ -57,6 +57,8 @@ struct BlockHost {
   double* xnext = nullptr;   // AMM carried next proposal [K][DP] (samplers.h amm)
   int64_t* xtag = nullptr;   // AMM [K] tag of the carried proposal
   uint64_t* astat = nullptr; // AMM [K][MMB_AMM_STAT_STRIDE] factorization counters (mmb_amm_stats)
+  int32_t* sep_d = nullptr;  // node-IR AMWG: coordinate -> element-term table (ir_sep_table), engine lifetime
+  double sep_eps = 0.0;
 };
 
 struct mmb_engine {
@@ -163,6 +165,83 @@ static int node_dim(const mmb_model_spec& s, const mmb_ir_model* ir, int node, b
 }
 
 static int tri(int i) { return i * (i + 1) / 2; }
+
+// ---- node IR: AMWG blocks whose logpdf! separates by coordinate (lane-parallel decisions) ----
+// amwg_sub! (amwg.jl:99-115) evaluates logpdf!(m, x, block) once per coordinate.  The block's
+// terms (simulation.jl:77-90) are sums over node elements (logpdf_sub, distributionstruct.jl:
+// 136-168); when every element's term reads at most one coordinate of the block -- through the
+// node's own value or a parameter expression's VAL / VALI / VALG slot -- coordinate j's two
+// evaluations differ exactly in the terms of the elements that read j, whatever the accept
+// history of the other coordinates, so every coordinate's difference can be formed at once (ir.h
+// amwg_dm, samplers.h amwg_lanes).  The table lists, per coordinate, the (term, element) pairs
+// that read it, then the pairs that read none; an MvNormal term's sigma must read none.  The
+// gather indices are data, so this is built per engine at upload, not in the JIT source.
+static void ir_expr_slots(const std::vector<int32_t>& code, const std::vector<double>& pool, int pc, int i,
+                          std::vector<int>& slots) {
+  for (;; ++pc) {
+    const int w = code[pc];
+    const int op = (int)((uint32_t)w >> 24), arg = w & 0xffffff;
+    if (op == MMB_IR_OP_END) return;
+    if (op == MMB_IR_OP_VAL) slots.push_back(arg);
+    else if (op == MMB_IR_OP_VALI) slots.push_back(arg + i);
+    else if (op == MMB_IR_OP_VALG) slots.push_back(arg + (int)pool[code[++pc] + i]);
+  }
+}
+static bool ir_sep_table(const std::vector<mmb_ir_node>& nodes, const std::vector<int32_t>& code,
+                         const std::vector<double>& pool, const mmb_ir_block& IB, const mmb_block_spec& s,
+                         int nvalues, std::vector<int32_t>& tab, double* epsf) {
+  std::vector<int> coord((size_t)nvalues, -1);
+  int d = 0;
+  for (int a = 0; a < s.nnodes; ++a) {
+    const mmb_ir_node& N = nodes[s.nodes[a]];
+    for (int q = 0; q < N.len; ++q) coord[N.off + q] = d + q;
+    d += N.len;
+  }
+  if (d < 2 || d > 32) return false;
+  std::vector<std::vector<int32_t>> lists((size_t)d + 1);
+  int nmax = 1;
+  size_t total = 0;
+  std::vector<int> sl;
+  for (int t = 0; t < IB.nterms; ++t) {
+    const mmb_ir_node& N = nodes[IB.term[t]];
+    const bool iso = N.family == MMB_IR_ISONORMAL;
+    if (iso) {  // sigma (at element 0) must not read the block
+      sl.clear();
+      ir_expr_slots(code, pool, N.expr[1], 0, sl);
+      for (int q : sl)
+        if (coord[q] >= 0) return false;
+    }
+    nmax = std::max(nmax, (N.len + 31) / 32);
+    for (int i = 0; i < N.len; ++i) {
+      sl.clear();
+      if (!N.fixed) sl.push_back(N.off + i);
+      for (int k = 0; k < (iso ? 1 : 2); ++k)
+        if (N.expr[k] >= 0) ir_expr_slots(code, pool, N.expr[k], i, sl);
+      int c = -1;
+      for (int q : sl) {
+        const int cq = coord[q];
+        if (cq < 0) continue;
+        if (c >= 0 && c != cq) return false;  // two coordinates: not separable
+        c = cq;
+      }
+      lists[c >= 0 ? c : d].push_back((int32_t)((t << 24) | i));
+      if (++total > (1u << 16)) return false;
+    }
+  }
+  tab.assign((size_t)d + 2, 0);
+  for (int j = 0; j <= d; ++j) {
+    tab[(size_t)j + 1] = tab[j] + (int32_t)lists[j].size();
+  }
+  for (int j = 0; j <= d; ++j) tab.insert(tab.end(), lists[j].begin(), lists[j].end());
+  // rounding band: each logf is a lane partial of <= nmax element terms, a 5-level butterfly, an
+  // MvNormal term's affine map and the sum over the terms, so it is within (nmax + nterms + 8) u
+  // of the exact sum of its element terms' magnitudes; 8x that, rounded up to a power of two
+  const int n = 8 * (nmax + IB.nterms + 8);
+  int e2 = 0;
+  while ((1 << e2) < n) ++e2;
+  *epsf = std::ldexp(1.0, e2 - 53);
+  return true;
+}
 
 static int tune_len_of(int kind, int d) {
   switch (kind) {
@@ -453,6 +532,17 @@ static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int d
     up(&e->d_ir_pool, e->ir_pool);
     up(&e->d_ir_mon, e->ir_mon);
     up(&e->d_ir_blocks, e->ir_blocks);
+    // AMWG blocks whose logpdf! separates by coordinate: lane-parallel decisions in the specialised
+    // kernel (MMB_IR_SEP=0 keeps every block on amwg_sub!'s sequential loop)
+    const char* se = std::getenv("MMB_IR_SEP");
+    const bool sep_on = !(se && std::string(se) == "0");
+    for (size_t b = 0; sep_on && b < e->blocks.size(); ++b) {
+      BlockHost& h = e->blocks[b];
+      std::vector<int32_t> tab;
+      if (h.spec.sampler == MMB_SAMPLER_AMWG &&
+          ir_sep_table(e->ir_nodes, e->ir_code, e->ir_pool, e->ir_blocks[b], h.spec, e->P, tab, &h.sep_eps))
+        up(&h.sep_d, tab);
+    }
     if (!ok) {
       mmb_destroy(e);
       return fail(nullptr, MMB_E_HIP, "node IR upload failed");
@@ -607,6 +697,13 @@ static void ir_jit_setup(mmb_engine* e, const mmb_model_spec* spec, const mmb_ir
   e->jit_mod = mod;
   e->jit_fn = fn;
   e->jit_info = "specialised kernel (" + info + ")";
+  int namwg = 0, nsep = 0;
+  for (const BlockHost& h : e->blocks)
+    if (h.spec.sampler == MMB_SAMPLER_AMWG) {
+      ++namwg;
+      nsep += h.sep_d != nullptr;
+    }
+  if (namwg) e->jit_info += "; lane-parallel AMWG blocks: " + std::to_string(nsep) + " of " + std::to_string(namwg);
 }
 
 int mmb_create_ir(const mmb_model_spec* spec, const mmb_ir_model* ir, int device, mmb_engine** out) {
@@ -716,6 +813,8 @@ void mmb_destroy(mmb_engine* e) {
     void* ip[] = {e->d_ir_nodes, e->d_ir_code, e->d_ir_mon, e->d_ir_const, e->d_ir_pool, e->d_ir_blocks};
     for (void* q : ip)
       if (q) (void)hipFree(q);
+    for (BlockHost& h : e->blocks)
+      if (h.sep_d) (void)hipFree(h.sep_d);
   }
   if (e->lg_X) (void)hipFree(e->lg_X);
   if (e->lg_y) (void)hipFree(e->lg_y);
@@ -892,6 +991,8 @@ static int upload_blocks(mmb_engine* e) {
     d.t_astat = h.astat;
     d.t_hmc = h.hmc;
     d.ir_blk = (int32_t)b;
+    d.sep = h.sep_d;
+    d.sep_eps = h.sep_eps;
   }
   if (!e->d_blocks) HIPCHK(e, hipMalloc(&e->d_blocks, MMB_MAX_BLOCKS * sizeof(DBlock)));
   HIPCHK(e, hipMemcpy(e->d_blocks, db.data(), db.size() * sizeof(DBlock), hipMemcpyHostToDevice));

@@ -201,12 +201,117 @@ struct Mdl<MMB_MODEL_IR> {
     put(B, s, g.lane, x, s.cur, s.prop);
   }
 
-  static constexpr bool AMWG_SEP = false;  // samplers.h amwg: sequential path only
-  static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
-  static constexpr int SLICE_CAND_D = 1;
   struct SCtx {};
   struct SMemo {};
   struct Prep {};
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SEP)
+  // Specialised kernels of schemes with AMWG: blocks whose logpdf! separates by coordinate
+  // (engine.cpp ir_sep_table; B.sep) decide every coordinate at once (samplers.h amwg_lanes)
+  static constexpr bool AMWG_SEP = true;
+#else
+  static constexpr bool AMWG_SEP = false;  // samplers.h amwg: sequential path only
+#endif
+  static constexpr bool AMWG_PROBE = false;  // (the near-threshold test hook is rats-only)
+  __device__ __forceinline__ static bool amwg_sep(const DBlock& B) { return B.sep != nullptr; }
+  __device__ __forceinline__ static bool slice_cand_ok(const DBlock& B) { return B.d <= SLICE_CAND_D; }
+  __device__ __forceinline__ static void slice_cand_prep(const SweepArgs&, const DBlock&, const St&, const Lc&,
+                                                         const Grp<G>&, double*, SCtx&) {}
+  // logpdf!(m, x, block) at the candidate xv (this lane's 8-lane group's), as logf: xv relisted
+  // (invlinked when transformed, put()) into the coordinates' state values
+  __device__ __forceinline__ static double slice_cand_logf(const SweepArgs& A, const DBlock& B, const St& s,
+                                                           const SCtx&, const double* xv, int lane, SMemo&) {
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
+    double c[SLICE_CAND_D];
+#pragma unroll
+    for (int a = 0; a < SLICE_CAND_D; ++a) {
+      c[a] = 0.0;
+      if (a < B.d) {
+        int lk;
+        double lo, hi;
+        (void)elem(s, B, a, &lk, &lo, &hi);
+        c[a] = B.transform ? mmb_ir_invlink(lk, xv[a], lo, hi) : xv[a];
+      }
+    }
+    return mmb_jit_slice_cand(A, B.ir_blk, s.cur, c, lane & 7, B.transform);
+#else
+    (void)A; (void)B; (void)s; (void)xv; (void)lane;
+    return 0.0;
+#endif
+  }
+  __device__ __forceinline__ static double amwg_epsf(const DBlock& B) { return B.sep_eps; }
+  // Lane j: d_j = sum over the element terms that read coordinate j of w_t (e' - e), the exact
+  // difference of coordinate j's two logpdf! evaluations in amwg_sub! (the other terms are equal in
+  // both, whatever the other coordinates' accept history); w_t = 1, or -0.5 / sigma^2 for an
+  // MvNormal term (d_iso is affine in the sum of squares).  Every candidate is written into `prop`
+  // at once: an element reads at most one coordinate, so its term there is its term with only
+  // that coordinate moved.  epsm_j = M + sum_j |w| (|e'| + |e|) + |d_j|, M the sum over every element
+  // term of |w| max(|e|, |e'|) plus the MvNormal constants: each rounded logf is within
+  // (elements per lane + 5 + nterms + 3) u M of its exact value, and B.sep_eps is 8x that.
+  __device__ static void amwg_dm(const SweepArgs& A, const DBlock& B, const Prep&, const St& s, const Lc&,
+                                 const Grp<G>& g, double x0, double x1, double& del, double& epsm, bool& bad) {
+    (void)x0;
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SEP)
+    const double xx[1] = {x1};
+    put(B, s, g.lane, xx, s.prop, nullptr);
+    const int lane = g.lane, d = B.d;
+    const int32_t* T = B.sep;
+    const mmb_ir_block& IB = ir_const_ref(A.ir_blocks, B.ir_blk);
+    // term weights and MvNormal constants, term t on lane t, through the (unused) expression stack
+    double mloc = 0.0, nfc = 0.0;
+    if (lane < IB.nterms) {
+      double w, cst;
+      mmb_jit_termw(A, B.ir_blk, lane, s.cur, &w, &cst);
+      s.stk[lane] = w;
+      mloc = cst;
+      nfc = (isfinite(w) && isfinite(cst)) ? 0.0 : 1.0;
+    }
+    grp_sync();
+    double dsum = 0.0, sabs = 0.0;
+    bool nf = false;
+    if (lane < d) {
+      const int q1 = T[lane + 1];
+      for (int q = T[lane]; q < q1; ++q) {
+        const int ent = T[d + 2 + q];
+        const int t = ent >> 24, i = ent & 0xffffff;
+        const double w = s.stk[t];
+        const double eo = mmb_jit_elem(A, B.ir_blk, t, i, s.cur, B.transform);
+        const double en = mmb_jit_elem(A, B.ir_blk, t, i, s.prop, B.transform);
+        nf = nf || !isfinite(eo) || !isfinite(en);
+        dsum = dsum + w * (en - eo);
+        const double aw = fabs(w);
+        sabs = sabs + aw * (fabs(en) + fabs(eo));
+        mloc = mloc + aw * fmax(fabs(en), fabs(eo));
+      }
+    }
+    for (int q = T[d] + lane; q < T[d + 1]; q += G) {  // element terms that read no coordinate
+      const int ent = T[d + 2 + q];
+      const int t = ent >> 24, i = ent & 0xffffff;
+      const double eo = mmb_jit_elem(A, B.ir_blk, t, i, s.cur, B.transform);
+      nfc = isfinite(eo) ? nfc : 1.0;
+      mloc = mloc + fabs(s.stk[t]) * fabs(eo);
+    }
+    g.sum2(mloc, nfc);
+    grp_sync();  // the stack slots are free again
+    del = dsum;
+    epsm = mloc + sabs + fabs(dsum);
+    bad = nf || nfc != 0.0 || !isfinite(mloc);
+#else
+    (void)A; (void)B; (void)s; (void)g; (void)x1;
+    del = 0.0;
+    epsm = 0.0;
+    bad = true;
+#endif
+  }
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
+  // Specialised kernels: Slice blocks of up to four coordinates evaluate their shrink candidates
+  // four at a time, one per 8-lane group (samplers.h slice_uni_cand / slice_multi_cand), each
+  // through the generated mmb_jc_<block> (ir_jit.cpp gen_slice_cand: logf's own summation tree)
+  static constexpr bool SLICE_CAND = true;
+#else
+  static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
+#endif
+  static constexpr int SLICE_CAND_D = 4;
+  static constexpr int SLICE_NC = 4;
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   // logpdf!(m, x, block, transform)
   __device__ static double logf(const SweepArgs& A, const DBlock& B, const St& s, const Lc&, const Grp<G>& g,

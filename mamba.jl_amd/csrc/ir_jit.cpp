@@ -46,8 +46,17 @@ std::string lit(double v) {
 }
 
 // Emit the statements of expression `pc` (validated stack code, ends in END) evaluated at
-// element index `idx`; returns the temporary holding the value.
-std::string gen_expr(const mmb_ir_model& ir, int pc, const std::string& idx, std::ostringstream& o, int& tmp) {
+// element index `idx`; returns the temporary holding the value.  sub: state slots read from the
+// candidate values c[a] instead of vals (a Slice block's coordinates; run-time slots through the
+// generated reader rd(k)).
+std::string gen_expr(const mmb_ir_model& ir, int pc, const std::string& idx, std::ostringstream& o, int& tmp,
+                     const std::vector<int>* sub = nullptr) {
+  auto sval = [&](int slot) -> std::string {
+    if (sub)
+      for (size_t a = 0; a < sub->size(); ++a)
+        if ((*sub)[a] == slot) return "c[" + std::to_string(a) + "]";
+    return "vals[" + std::to_string(slot) + "]";
+  };
   std::vector<std::string> st;
   auto fresh = [&]() { return "t" + std::to_string(tmp++); };
   for (;; ++pc) {
@@ -57,11 +66,15 @@ std::string gen_expr(const mmb_ir_model& ir, int pc, const std::string& idx, std
     const std::string t = fresh();
     switch (op) {
       case MMB_IR_OP_CONST: o << "    const double " << t << " = " << lit(ir.consts[arg]) << ";\n"; break;
-      case MMB_IR_OP_VAL: o << "    const double " << t << " = vals[" << arg << "];\n"; break;
-      case MMB_IR_OP_VALI: o << "    const double " << t << " = vals[" << arg << " + " << idx << "];\n"; break;
+      case MMB_IR_OP_VAL: o << "    const double " << t << " = " << sval(arg) << ";\n"; break;
+      case MMB_IR_OP_VALI:
+        if (sub) o << "    const double " << t << " = rd(" << arg << " + " << idx << ");\n";
+        else o << "    const double " << t << " = vals[" << arg << " + " << idx << "];\n";
+        break;
       case MMB_IR_OP_VALG: {  // gather: the pool offset of the indices is the next word
         const int woff = ir.code[++pc];
-        o << "    const double " << t << " = vals[" << arg << " + (int)A.ir_pool[" << woff << " + " << idx << "]];\n";
+        if (sub) o << "    const double " << t << " = rd(" << arg << " + (int)A.ir_pool[" << woff << " + " << idx << "]);\n";
+        else o << "    const double " << t << " = vals[" << arg << " + (int)A.ir_pool[" << woff << " + " << idx << "]];\n";
         break;
       }
       case MMB_IR_OP_DATA: o << "    const double " << t << " = A.ir_pool[" << arg << " + " << idx << "];\n"; break;
@@ -117,6 +130,120 @@ void gen_node(const mmb_ir_model& ir, int n, std::ostringstream& o) {
   o << "  return g.sum(acc);\n}\n";
 }
 
+// One element's term of node n's logpdf_sub at element i, exactly as gen_node's loop forms it (the
+// lane-parallel AMWG of ir.h amwg_dm sums differences of these): mmb_ir_lp(...) for the element
+// families, r * r for an MvNormal (NaN when the value is not finite: its insupport test).
+void gen_elem(const mmb_ir_model& ir, int n, std::ostringstream& o) {
+  const mmb_ir_node& N = ir.nodes[n];
+  int tmp = 0;
+  o << "__device__ __forceinline__ double mmb_je_" << n << "(const SweepArgs& A, const double* vals, int i, int tr) {\n";
+  o << "  (void)tr; (void)A;\n";
+  const std::string src = N.fixed ? "(A.ir_pool + " + std::to_string(N.off) + ")" : "(vals + " + std::to_string(N.off) + ")";
+  if (N.family == MMB_IR_ISONORMAL) {
+    o << "  const double x = " << src << "[i];\n";
+    const std::string m = gen_expr(ir, N.expr[0], "i", o, tmp);
+    o << "  const double r = x - " << m << ";\n";
+    o << "  return isfinite(x) ? r * r : __builtin_nan(\"\");\n}\n";
+    return;
+  }
+  std::string a = "0.0", b = "0.0", ct = "0.0";
+  if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp);
+  if (N.expr[1] >= 0) b = gen_expr(ir, N.expr[1], "i", o, tmp);
+  if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
+  o << "  return mmb_ir_lp(" << N.family << ", " << src << "[i], " << a << ", " << b << ", " << ct << ", tr, "
+    << lit(N.lo) << ", " << lit(N.hi) << ");\n}\n";
+}
+
+// Weight of node n's element terms in the block's logpdf! and the magnitude of its constant part:
+// 1 and 0 for the element families; for an MvNormal, d_iso's -0.5 / sigma^2 and 0.5 |k log2pi +
+// k log sigma^2| (sigma at element 0, as gen_node evaluates it).
+void gen_termw(const mmb_ir_model& ir, int n, std::ostringstream& o) {
+  const mmb_ir_node& N = ir.nodes[n];
+  int tmp = 0;
+  o << "__device__ __forceinline__ void mmb_jw_" << n << "(const SweepArgs& A, const double* vals, double* w, double* c) {\n";
+  o << "  (void)A; (void)vals;\n";
+  if (N.family != MMB_IR_ISONORMAL) {
+    o << "  *w = 1.0;\n  *c = 0.0;\n}\n";
+    return;
+  }
+  o << "  const int i = 0;\n  (void)i;\n";
+  const std::string s = gen_expr(ir, N.expr[1], "i", o, tmp);
+  o << "  const double value = " << s << " * " << s << ";\n";
+  o << "  const double invv = 1.0 / value;\n";
+  o << "  *w = -0.5 * invv;\n";
+  o << "  *c = 0.5 * fabs(" << N.len << " * MMB_LOG2PI + " << N.len << " * mmb_log(value));\n}\n";
+}
+
+// logpdf!(m, x, block) of Slice block b at one candidate per 8-lane group (samplers.h
+// slice_uni_cand / slice_multi_cand; ir.h slice_cand_logf): the block's coordinates are read from
+// c[] (state values, invlinked) instead of the chain state.  Lane r of the group stands for lanes
+// 4r .. 4r+3 of the 32-lane layout: it forms their four lane partials (elements i = lane, lane + 32,
+// .. in order, as gen_node's loop) and combines them as levels 0-1 of the 32-lane butterfly, ((p0 +
+// p1) + (p2 + p3)); levels 2-4 are xor 1, 2, 4 across the group (DPP, as Grp<32>::sum's half-mirror
+// and mirror stages after quads agree).  The same tree over the same terms: bit-identical to logf.
+void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, std::ostringstream& o) {
+  const mmb_block_spec& s = spec.blocks[b];
+  const mmb_ir_block& IB = ir.blocks[b];
+  std::vector<int> slots;
+  for (int a = 0; a < s.nnodes; ++a) {
+    const mmb_ir_node& N = ir.nodes[s.nodes[a]];
+    for (int q = 0; q < N.len; ++q) slots.push_back(N.off + q);
+  }
+  o << "__device__ double mmb_jc_" << b << "(const SweepArgs& A, const double* vals, const double* c, int r,\n"
+       "                                        int transform) {\n";
+  o << "  (void)transform;\n";
+  o << "  auto rd = [&](int k) -> double {\n    return ";
+  for (size_t a = 0; a < slots.size(); ++a) o << "k == " << slots[a] << " ? c[" << a << "] : ";
+  o << "vals[k];\n  };\n  (void)rd;\n";
+  o << "  double lp = 0.0;\n";
+  int tmp = 0;
+  for (int t = 0; t < IB.nterms; ++t) {
+    const int n = IB.term[t];
+    const mmb_ir_node& N = ir.nodes[n];
+    bool inblk = false;
+    for (int a = 0; a < s.nnodes; ++a) inblk = inblk || s.nodes[a] == n;
+    const std::string tr = IB.trans[t] ? "transform" : "0";
+    auto xval = [&](const std::string& i) {
+      if (N.fixed) return "A.ir_pool[" + std::to_string(N.off) + " + " + i + "]";
+      if (inblk) return "rd(" + std::to_string(N.off) + " + " + i + ")";
+      return "vals[" + std::to_string(N.off) + " + " + i + "]";
+    };
+    o << "  {  // term " << t << ": node " << n << "\n";
+    if (N.family == MMB_IR_ISONORMAL) {
+      o << "    double sig;\n    {\n    const int i = 0;\n    (void)i;\n";
+      const std::string sg = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
+      o << "    sig = " << sg << ";\n    }\n";
+      o << "    double p[4], bd = 0.0;\n";
+      o << "#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      double ss = 0.0;\n";
+      o << "      for (int i = 4 * r + v; i < " << N.len << "; i += 32) {\n";
+      o << "        const double x = " << xval("i") << ";\n";
+      const std::string m = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
+      o << "        const double rr = x - " << m << ";\n        ss = ss + rr * rr;\n";
+      o << "        bd = isfinite(x) ? bd : 1.0;\n      }\n      p[v] = ss;\n    }\n";
+      o << "    double sv = (p[0] + p[1]) + (p[2] + p[3]);\n";
+      o << "    sv += Grp<32>::other_d<0>(sv); bd += Grp<32>::other_d<0>(bd);\n";
+      o << "    sv += Grp<32>::other_d<1>(sv); bd += Grp<32>::other_d<1>(bd);\n";
+      o << "    sv += Grp<32>::other_d<2>(sv); bd += Grp<32>::other_d<2>(bd);\n";
+      o << "    lp += bd != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, sv);\n";
+    } else {
+      o << "    double p[4];\n";
+      o << "#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      double acc = 0.0;\n";
+      o << "      for (int i = 4 * r + v; i < " << N.len << "; i += 32) {\n";
+      std::string a = "0.0", bb = "0.0", ct = "0.0";
+      if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
+      if (N.expr[1] >= 0) bb = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
+      if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
+      o << "        acc = acc + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
+        << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n      }\n      p[v] = acc;\n    }\n";
+      o << "    double sv = (p[0] + p[1]) + (p[2] + p[3]);\n";
+      o << "    sv += Grp<32>::other_d<0>(sv);\n    sv += Grp<32>::other_d<1>(sv);\n    sv += Grp<32>::other_d<2>(sv);\n";
+      o << "    lp += sv;\n";
+    }
+    o << "    if (!isfinite(lp)) return lp;\n  }\n";
+  }
+  o << "  return lp;\n}\n";
+}
+
 uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
   const unsigned char* c = (const unsigned char*)p;
   for (size_t i = 0; i < n; ++i) { h ^= c[i]; h *= 1099511628211ull; }
@@ -169,6 +296,70 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
     o << "      break;\n";
   }
   o << "    default: break;\n  }\n  return lp;\n}\n";
+  if (kinds & (1u << MMB_SAMPLER_AMWG)) {
+    // element terms and term weights of the AMWG blocks' logpdf! (lane-parallel decisions, ir.h
+    // amwg_dm; used only on blocks the engine finds separable, engine.cpp ir_sep_table)
+    std::vector<char> en(ir.nnodes, 0);
+    for (int b = 0; b < spec.nblocks; ++b)
+      if (spec.blocks[b].sampler == MMB_SAMPLER_AMWG)
+        for (int t = 0; t < ir.blocks[b].nterms; ++t) en[ir.blocks[b].term[t]] = 1;
+    for (int n = 0; n < ir.nnodes; ++n)
+      if (en[n]) {
+        gen_elem(ir, n, o);
+        gen_termw(ir, n, o);
+      }
+    o << "#define MMB_IR_SEP 1\n";
+    o << "__device__ __forceinline__ double mmb_jit_elem(const SweepArgs& A, int blk, int t, int i, const double* vals,\n"
+         "                                               int transform) {\n"
+         "  (void)transform;\n  switch (blk) {\n";
+    for (int b = 0; b < spec.nblocks; ++b) {
+      if (spec.blocks[b].sampler != MMB_SAMPLER_AMWG) continue;
+      const mmb_ir_block& IB = ir.blocks[b];
+      o << "    case " << b << ":\n      switch (t) {\n";
+      for (int t = 0; t < IB.nterms; ++t)
+        o << "        case " << t << ": return mmb_je_" << IB.term[t] << "(A, vals, i, "
+          << (IB.trans[t] ? "transform" : "0") << ");\n";
+      o << "        default: return 0.0;\n      }\n";
+    }
+    o << "    default: return 0.0;\n  }\n}\n";
+    o << "__device__ __forceinline__ void mmb_jit_termw(const SweepArgs& A, int blk, int t, const double* vals,\n"
+         "                                              double* w, double* c) {\n"
+         "  *w = 1.0;\n  *c = 0.0;\n  switch (blk) {\n";
+    for (int b = 0; b < spec.nblocks; ++b) {
+      if (spec.blocks[b].sampler != MMB_SAMPLER_AMWG) continue;
+      const mmb_ir_block& IB = ir.blocks[b];
+      o << "    case " << b << ":\n      switch (t) {\n";
+      for (int t = 0; t < IB.nterms; ++t)
+        o << "        case " << t << ": mmb_jw_" << IB.term[t] << "(A, vals, w, c); return;\n";
+      o << "        default: return;\n      }\n";
+    }
+    o << "    default: return;\n  }\n}\n";
+  }
+  {  // Slice blocks of up to four coordinates: candidates evaluated four at a time (ir.h)
+    bool any = false;
+    for (int b = 0; b < spec.nblocks; ++b) {
+      if (spec.blocks[b].sampler != MMB_SAMPLER_SLICE) continue;
+      int d = 0;
+      for (int a = 0; a < spec.blocks[b].nnodes; ++a) d += ir.nodes[spec.blocks[b].nodes[a]].len;
+      if (d > 4) continue;
+      gen_slice_cand(spec, ir, b, o);
+      any = true;
+    }
+    if (any) {
+      o << "#define MMB_IR_SLICEC 1\n";
+      o << "__device__ __forceinline__ double mmb_jit_slice_cand(const SweepArgs& A, int blk, const double* vals,\n"
+           "                                                     const double* c, int r, int transform) {\n"
+           "  switch (blk) {\n";
+      for (int b = 0; b < spec.nblocks; ++b) {
+        if (spec.blocks[b].sampler != MMB_SAMPLER_SLICE) continue;
+        int d = 0;
+        for (int a = 0; a < spec.blocks[b].nnodes; ++a) d += ir.nodes[spec.blocks[b].nodes[a]].len;
+        if (d > 4) continue;
+        o << "    case " << b << ": return mmb_jc_" << b << "(A, vals, c, r, transform);\n";
+      }
+      o << "    default: return __builtin_nan(\"\");\n  }\n}\n";
+    }
+  }
   // monitored Logical nodes (write_draws)
   o << "__device__ __forceinline__ double mmb_jit_logical(const SweepArgs& A, int n, int i, const double* vals) {\n"
        "  (void)A; (void)i; (void)vals;\n  switch (n) {\n";

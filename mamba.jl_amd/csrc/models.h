@@ -217,9 +217,27 @@ struct Mdl<MMB_MODEL_RATS> {
     tp = normsum_lane(c.mu, c.sig, c.logsig, xa, lane);
     ts = c.al ? ssr_lane(A, l, xa, s.b, lane) : ssr_lane(A, l, s.a, xa, lane);
   }
-  // logf_vec = (0 + sum tp) + (-0.5 * (yk + (sum ts) * invv))
-  __device__ __forceinline__ static double amwg_yk(const VecCtx& c) { return c.yk; }
-  __device__ __forceinline__ static double amwg_invv(const VecCtx& c) { return c.invv; }
+  // logf_vec = (0 + sum tp) + (-0.5 * (yk + (sum ts) * invv)).  Coordinate j's exact difference
+  // d_j = (tp_j' - tp_j) - 0.5 invv (ts_j' - ts_j); each rounded logf is within 9 u (sum_i |tp_i| +
+  // |yk| + invv sum_i |ts_i|) of its exact value (a depth-5 tree sum, then three roundings):
+  // band = 2^-46 (128 u) times that magnitude plus the difference's own terms (samplers.h amwg_lanes)
+  static constexpr bool AMWG_PROBE = true;
+  __device__ __forceinline__ static double amwg_epsf(const DBlock&) { return 0x1p-46; }
+  __device__ __forceinline__ static void amwg_dm(const SweepArgs& A, const DBlock&, const VecCtx& c, const St& s,
+                                                 const Lc& l, const Grp<G>& g, double x0, double x1, double& del,
+                                                 double& epsm, bool& bad) {
+    double tp0, ts0, tp1, ts1;
+    amwg_terms(A, c, s, l, g.lane, x0, tp0, ts0);
+    amwg_terms(A, c, s, l, g.lane, x1, tp1, ts1);
+    bad = !(isfinite(tp0) && isfinite(ts0) && isfinite(tp1) && isfinite(ts1));
+    double ap = fmax(fabs(tp0), fabs(tp1)), as = fmax(fabs(ts0), fabs(ts1));
+    g.sum2(ap, as);  // bounds of sum |terms| over both states
+    const double dp = tp1 - tp0, ds = ts1 - ts0;
+    del = dp + (-0.5 * c.invv) * ds;
+    const double mag = ap + fabs(c.yk) + c.invv * as;
+    epsm = mag + fabs(dp) + c.invv * fabs(ds) + fabs(del);
+    bad = bad || !isfinite(c.invv) || !isfinite(c.yk);
+  }
   // block-update-invariant context (vector blocks); scalar blocks fall back to logf
   using Prep = VecCtx;
   __device__ __forceinline__ static Prep prep(const DBlock& B, const St& s) { return vec_ctx(B, s); }

@@ -83,30 +83,26 @@ struct Smp {
   // accept counts as the sequential loop, bit for bit, since certain decisions are its
   // decisions.  Any uncertain lane, a non-finite term or bound: false, and the caller runs
   // the sequential loop (RNG draws are the same precomputed z / uown either way).
+  // The model gives, per lane j, d_j and the magnitude epsm_j its rounding band scales with
+  // (M::amwg_dm: rats models.h, the node IR's separable blocks ir.h), and the band's relative
+  // factor (M::amwg_epsf).
   __device__ __forceinline__ static bool amwg_lanes(const DBlock& B, const typename M::Prep& pc, const St& s,
                                                     const Lc& l, const Grp<G>& g, double* x, const double* z,
                                                     const double* uown, double* acc, double ad,
                                                     const SweepArgs& A) {
     const bool in = g.lane < B.d;
     const double x1 = x[0] + z[0];  // the sequential loop's x[r] += z[r]
-    double tp0, ts0, tp1, ts1;
-    M::amwg_terms(A, pc, s, l, g.lane, x[0], tp0, ts0);
-    M::amwg_terms(A, pc, s, l, g.lane, x1, tp1, ts1);
-    const double invv = M::amwg_invv(pc), yk = M::amwg_yk(pc);
-    bool bad = !(isfinite(tp0) && isfinite(ts0) && isfinite(tp1) && isfinite(ts1));
-    double ap = fmax(fabs(tp0), fabs(tp1)), as = fmax(fabs(ts0), fabs(ts1));
-    g.sum2(ap, as);  // bounds of sum |terms| over both states
-    const double dp = tp1 - tp0, ds = ts1 - ts0;
-    const double del = dp + (-0.5 * invv) * ds;
-    const double mag = ap + fabs(yk) + invv * as;
+    double del, epsm;
+    bool bad;
+    M::amwg_dm(A, B, pc, s, l, g, x[0], x1, del, epsm, bad);
     // (amwg_exact = 2, tests: a 2^30 times wider band, so that many updates fall back)
-    const double eps = (A.amwg_exact == 2 ? 0x1p-16 : 0x1p-46) * (mag + fabs(dp) + invv * fabs(ds) + fabs(del));
+    const double eps = (A.amwg_exact == 2 ? 0x1p30 * M::amwg_epsf(B) : M::amwg_epsf(B)) * epsm;
     const double lo = del - eps, hi = del + eps;
     const double ue = uown[0];  // in [0, 1)
     const bool acc_c = lo >= 700.0 || (lo > -700.0 && ue < mmb_exp(lo) * (1.0 - 0x1p-48));
     const bool rej_c = (hi <= -700.0 && ue >= 1e-300) ||
                        (hi > -700.0 && hi < 700.0 && ue >= mmb_exp(hi) * (1.0 + 0x1p-48));
-    bad = bad || !isfinite(eps) || !isfinite(invv) || !isfinite(yk);
+    bad = bad || !isfinite(eps);
     const bool unsure = in && (bad || !(acc_c || rej_c));
     const uint64_t bal = __ballot(unsure);
     const bool any = (threadIdx.x & 32) ? (bal >> 32) != 0 : (uint32_t)bal != 0;
@@ -154,14 +150,13 @@ struct Smp {
     }
     bool seq = true;
     if constexpr (M::AMWG_SEP && G == 32 && R == 1) {
-      if (A.amwg_probe != 0 && M::amwg_sep(B)) {
-        // test-only (MMB_AMWG_PROBE=1): uniforms a few ulps to 2^-12 off each coordinate's accept
-        // threshold exp(d_j) (mmb_math.h mmb_amwg_probe_factor; the oracle draws the same), so
-        // both the lane-parallel decision and its sequential fallback meet near-ties
-        double tp0, ts0, tp1, ts1;
-        M::amwg_terms(A, pc, s, l, g.lane, x[0], tp0, ts0);
-        M::amwg_terms(A, pc, s, l, g.lane, x[0] + z[0], tp1, ts1);
-        const double del = (tp1 - tp0) + (-0.5 * M::amwg_invv(pc)) * (ts1 - ts0);
+      if (M::AMWG_PROBE && A.amwg_probe != 0 && M::amwg_sep(B)) {
+        // test-only (MMB_AMWG_PROBE=1, rats): uniforms a few ulps to 2^-12 off each coordinate's
+        // accept threshold exp(d_j) (mmb_math.h mmb_amwg_probe_factor; the oracle draws the same),
+        // so both the lane-parallel decision and its sequential fallback meet near-ties
+        double del, em;
+        bool bd;
+        M::amwg_dm(A, B, pc, s, l, g, x[0], x[0] + z[0], del, em, bd);
         uown[0] = g.lane < d ? mmb_amwg_probe_uniform(del, &ru, (uint32_t)g.lane) : 0.0;
       }
       if (A.amwg_exact != 1 && M::amwg_sep(B)) {

@@ -103,6 +103,44 @@ def test_ir_gpu_vs_oracle(mamba, oracle, case, kernel, monkeypatch):
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
 
 
+@pytest.mark.parametrize("name", ["rats", "seeds", "blocker"])
+def test_ir_lane_parallel_amwg(mamba, oracle, name, monkeypatch):
+    """AMWG blocks whose logpdf! separates by coordinate (engine.cpp ir_sep_table: every element
+    term reads at most one coordinate -- rats alpha / beta through the y gather, seeds b, blocker
+    delta) decide all coordinates at once in the specialised kernel (ir.h amwg_dm); the draws,
+    values and tune equal the one-coordinate-at-a-time loop (MMB_IR_SEP=0), the band-widened mode
+    (MMB_AMWG_EXACT=2, many fallbacks) and the oracle bit for bit, and the fallback is rare."""
+    if name == "rats":
+        m = mamba.ir.rats_model().setinputs(mamba.ir.rats_inputs()).setsamplers(mamba.model.rats_scheme_reference())
+        V = m.init_matrix([{**mamba.model.RATS_INITS[k % 2], "y": mamba.model.RATS_Y} for k in range(256)], 256)
+        nsep = 2
+    else:
+        m, V = example(mamba, name, 256)
+        nsep = 1 if name == "seeds" else 2  # seeds: b (s2 is one coordinate); blocker: mu, [delta, delta_new]
+    out, seq = {}, {}
+    for mode in ("sep", "sequential", "wide"):
+        monkeypatch.setenv("MMB_IR_SEP", "0" if mode == "sequential" else "1")
+        monkeypatch.setenv("MMB_AMWG_EXACT", "2" if mode == "wide" else "0")
+        eng = mamba.Engine(m)
+        jit, info = eng.ir_jit()
+        assert jit, info
+        if mode != "sequential":
+            assert f"lane-parallel AMWG blocks: {nsep} of" in info, info
+        eng.init_chains(V, seed=23)
+        d = eng.run(80, burnin=20, thin=2)
+        out[mode] = (d, eng.values(), eng.tune())
+        seq[mode] = eng.amwg_stats()["sequential_updates"]
+    st = oracle.new_state(m, V)
+    do = oracle.run(m, st, 80, burnin=20, thin=2, seed=23, nthreads=8)
+    for mode in out:
+        np.testing.assert_array_equal(out[mode][0], do)
+        np.testing.assert_array_equal(out[mode][1], st["values"])
+        np.testing.assert_array_equal(out[mode][2], st["tune"][:, :st["tl"]])
+    updates = nsep * V.shape[0] * 80
+    assert seq["sep"] <= 0.01 * updates, (seq, updates)
+    assert seq["wide"] > seq["sep"], seq
+
+
 def test_ir_rats_reference_scheme_gpu_vs_oracle(mamba, oracle, monkeypatch):
     """rats through the node IR with the reference Slice + AMWG scheme (rats.jl:112-116): the
     specialised kernel, the interpreter and the oracle agree bit for bit."""
