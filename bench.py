@@ -71,6 +71,9 @@ def parse():
                    help="logistic: Model.burnin of the timed run (default steps // 2: 1000 of 2000)")
     p.add_argument("--scheme", default="gibbs_amm",
                    help="gibbs_amm (metric config) | reference | ablations: amm_noadapt, gibbs_only")
+    p.add_argument("--gradient", default="analytic", choices=["analytic", "forward"],
+                   help="logistic: the analytic gradient kernel, or the reference's default dtype=:forward "
+                        "(Calculus forward differences: p + 1 log-density columns per gradient)")
     p.add_argument("--amm-fullrank", action="store_true",
                    help="ablation (rats gibbs_amm): AMM moments seeded positive definite, so every "
                         "factorization reaches full rank (no amm.jl:102 alias chains)")
@@ -221,12 +224,14 @@ def setup_workload(mb, args, rank):
     data, _ = mb.model.logistic_data(10000, 50)
     model = mb.logistic(10000, 50, 10.0)
     model.setinputs(data)
-    # the logistic kernel's gradient is the analytic one, asked for explicitly: the reference's
-    # default dtype=:forward (Calculus) is refused by mmb_create (MMB_E_UNSUPPORTED)
-    model.setsamplers([mb.NUTS("beta", dtype="analytic")])
+    # gradient: the analytic kernel (dtype=:analytic, asked for explicitly), or the reference's
+    # default dtype=:forward -- Calculus forward differences, 51 log-density columns per gradient
+    model.setsamplers([mb.NUTS("beta", dtype=args.gradient)])
     init = np.random.default_rng(1000 + rank).normal(0.0, 0.1, (K, 50))
-    return (model, init, "logistic N=10000 p=50 NUTS (BASELINE configs[3]), analytic gradient (dtype=:analytic; "
-            "the reference default :forward is refused by this kernel)", {"thin": 1}, "f64")
+    what = ("analytic gradient (dtype=:analytic)" if args.gradient == "analytic" else
+            "the reference's default gradient dtype=:forward (Calculus forward differences, 51 logpdf! "
+            "columns per gradient on the MFMA kernel)")
+    return (model, init, f"logistic N=10000 p=50 NUTS (BASELINE configs[3]), {what}", {"thin": 1}, "f64")
 
 
 def amm_window(model, before, after):
@@ -455,7 +460,9 @@ def main():
         # measured over the timed window itself (the config's whole 2000-iteration run): its
         # gradient count and the HIP-event time of its gradient launches
         kms, launches = t_kms, t_launches
-        flops = 4.0 * 10000 * 50 * grads_timed
+        # forward differences: 51 columns of X * beta' (2 N p flops each), no X' res
+        per_grad = 4.0 * 10000 * 50 if args.gradient == "analytic" else 2.0 * 10000 * 50 * 51
+        flops = per_grad * grads_timed
         achieved = flops / (kms * 1e-3) / 1e12
         # the same flops over the window's wall time: the gradient launches are 77 % of it, the
         # control kernel (NUTS machines, partial folding) 22 %, launch gaps 0.5 % (rocprofv3 trace,
@@ -464,7 +471,7 @@ def main():
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None,
                 "achieved_wall": wall_tfs, "frac_wall": wall_tfs / F64_MFMA_PEAK_TFS,
-                "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": 4.0 * 10000 * 50,
+                "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": per_grad,
                 "avg_launch_ms": kms / launches, "gradients_per_launch": grads_timed / launches,
                 "gradients_per_chain_update_timed": grads_timed / (K * args.steps),
                 "window": f"timed run: {args.steps} iterations, burnin {tburn}"}
@@ -530,6 +537,8 @@ def main():
     }
     if args.workload != "rats":
         out["metric"] = f"chain-updates/sec on {args.workload} (not the headline metric)"
+    if nuts:
+        out["config"]["gradient"] = args.gradient
     if args.workload == "rats":
         out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "16")),
                               "scheme": args.scheme})

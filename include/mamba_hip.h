@@ -98,8 +98,8 @@ typedef enum { MMB_SLICE_MULTIVARIATE = 0, MMB_SLICE_UNIVARIATE = 1 } mmb_slice_
  *                     reference's), the analytic gradient kernel on logistic (configs[3]) --
  *                     C callers only; the Python mirror and the Julia shim pass FORWARD or
  *                     ANALYTIC explicitly, so the substitution is never implicit
- *   MMB_GRAD_FORWARD  forward differences (line, node IR; logistic: MMB_E_UNSUPPORTED, the
- *                     caller keeps the reference path)
+ *   MMB_GRAD_FORWARD  forward differences (line, node IR, logistic: p + 1 log-density columns
+ *                     per gradient through the batched MFMA kernel, ABI 9)
  *   MMB_GRAD_ANALYTIC the hand-derived gradient (line, logistic; node IR: MMB_E_ARG) */
 typedef enum { MMB_GRAD_DEFAULT = 0, MMB_GRAD_FORWARD = 1, MMB_GRAD_ANALYTIC = 2 } mmb_gradient;
 

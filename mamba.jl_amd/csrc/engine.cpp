@@ -81,6 +81,7 @@ struct mmb_engine {
   DBlock* d_blocks = nullptr;
   // logistic (config 4): padded X/y and the NUTS machine state (logistic.h)
   int lg_N = 0, lg_p = 0, lg_rps = 0;
+  bool lg_fd = false;  // forward-difference gradient (MMB_GRAD_FORWARD): p + 1 columns per request
   double *lg_X = nullptr, *lg_y = nullptr;
   double *lg_vec = nullptr, *lg_sc = nullptr, *lg_frames = nullptr, *lg_pos = nullptr;
   double *lg_gpart = nullptr, *lg_lpart = nullptr;
@@ -412,15 +413,10 @@ static int create_impl(const mmb_model_spec* spec, const mmb_ir_model* ir, int d
     // model supports them (line, node IR), the analytic gradient on line and logistic
     if (s.sampler == MMB_SAMPLER_NUTS || s.sampler == MMB_SAMPLER_HMC || s.sampler == MMB_SAMPLER_MALA) {
       const int gr = s.gradient;
-      if (gr == MMB_GRAD_FORWARD && e->model == MMB_MODEL_LOGISTIC) {
-        // the reference's default dtype=:forward (Calculus forward differences, simulation.jl:47-51)
-        // is not on the logistic kernel: refused explicitly (the caller keeps the Julia path or
-        // asks for the analytic gradient), never silently replaced
-        delete e;
-        return fail(nullptr, MMB_E_UNSUPPORTED,
-                    "block %d: logistic has no forward-difference gradient kernel (dtype=:forward); "
-                    "use dtype=:analytic (MMB_GRAD_ANALYTIC) for the batched analytic gradient", b);
-      }
+      // logistic: the reference's default dtype=:forward (Calculus forward differences,
+      // simulation.jl:47-51) runs as p + 1 log-density columns per request through the batched
+      // MFMA kernel (logistic.hip lg_grad_kernel<.., LPONLY>, lg_assemble_fd)
+      if (e->model == MMB_MODEL_LOGISTIC) e->lg_fd = gr == MMB_GRAD_FORWARD;
       const bool ok = gr == MMB_GRAD_DEFAULT || gr == MMB_GRAD_FORWARD ||
                       (gr == MMB_GRAD_ANALYTIC && e->model != MMB_MODEL_IR);
       if (!ok) {
@@ -1089,7 +1085,7 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     HIPCHK(e, dalloc(&e->lg_frames, (size_t)K * NutsFrames<MMB_LG_DV>::DBL));
     HIPCHK(e, dalloc(&e->lg_pos, (size_t)K * MMB_LG_DV));
     HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NG * MMB_LG_NS * K * MMB_LG_DV));
-    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * MMB_LG_NS * K));
+    HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * MMB_LG_NS * K * (e->lg_fd ? e->lg_p + 1 : 1)));
     HIPCHK(e, dalloc(&e->lg_count, 2));
     HIPCHK(e, dalloc(&e->lg_s2c, (size_t)2 * K));
     HIPCHK(e, dalloc(&e->lg_ngrad, 1));
@@ -1249,6 +1245,9 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
   A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count; A.s2c = e->lg_s2c;
   A.ngrad = e->lg_ngrad;
   A.nstat = e->d_nstat;
+  A.fd = e->lg_fd ? 1 : 0;
+  A.nv = e->lg_fd ? e->lg_p + 1 : 1;
+  A.Kv = e->K * A.nv;
   HIPCHK(e, hipMemsetAsync(e->lg_ngrad, 0, sizeof(unsigned long long), e->stream));
   e->kernel_ms = 0.0;
   e->launches = 0;
@@ -1287,7 +1286,7 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
       // group mode once the step is wide enough to fill the GPU with one workgroup per
       // (group, 64-chain tile): half the partial traffic; one workgroup per sub-range below
       // that, where a step's latency is what counts
-      const int fold = nbound >= MMB_LG_FOLD_MIN ? 1 : 0;
+      const int fold = (int64_t)nbound * A.nv >= MMB_LG_FOLD_MIN ? 1 : 0;
       st = mmb_lg_launch_grad(A, par, nbound, fold, e->stream);
       if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_grad launch: %s", hipGetErrorString(st));
       if (a->time_kernels) HIPCHK(e, hipEventRecord(ev[2 * s + 1], e->stream));

@@ -310,7 +310,7 @@ struct Mdl<MMB_MODEL_IR> {
 #else
   static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
 #endif
-  static constexpr int SLICE_CAND_D = 4;
+  static constexpr int SLICE_CAND_D = 2;
   static constexpr int SLICE_NC = 4;
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   // logpdf!(m, x, block, transform)

@@ -23,6 +23,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -189,7 +190,7 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, s
     const mmb_ir_node& N = ir.nodes[s.nodes[a]];
     for (int q = 0; q < N.len; ++q) slots.push_back(N.off + q);
   }
-  o << "__device__ double mmb_jc_" << b << "(const SweepArgs& A, const double* vals, const double* c, int r,\n"
+  o << "__device__ __forceinline__ double mmb_jc_" << b << "(const SweepArgs& A, const double* vals, const double* c, int r,\n"
        "                                        int transform) {\n";
   o << "  (void)transform;\n";
   o << "  auto rd = [&](int k) -> double {\n    return ";
@@ -213,29 +214,31 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, s
       o << "    double sig;\n    {\n    const int i = 0;\n    (void)i;\n";
       const std::string sg = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
       o << "    sig = " << sg << ";\n    }\n";
-      o << "    double p[4], bd = 0.0;\n";
-      o << "#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      double ss = 0.0;\n";
+      o << "    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0, bd = 0.0;\n";
+      o << "#pragma nounroll\n    for (int v = 0; v < 4; ++v) {\n      double ss = 0.0;\n";
       o << "      for (int i = 4 * r + v; i < " << N.len << "; i += 32) {\n";
       o << "        const double x = " << xval("i") << ";\n";
       const std::string m = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
       o << "        const double rr = x - " << m << ";\n        ss = ss + rr * rr;\n";
-      o << "        bd = isfinite(x) ? bd : 1.0;\n      }\n      p[v] = ss;\n    }\n";
-      o << "    double sv = (p[0] + p[1]) + (p[2] + p[3]);\n";
+      o << "        bd = isfinite(x) ? bd : 1.0;\n      }\n";
+      o << "      p0 = v == 0 ? ss : p0;\n      p1 = v == 1 ? ss : p1;\n      p2 = v == 2 ? ss : p2;\n      p3 = v == 3 ? ss : p3;\n    }\n";
+      o << "    double sv = (p0 + p1) + (p2 + p3);\n";
       o << "    sv += Grp<32>::other_d<0>(sv); bd += Grp<32>::other_d<0>(bd);\n";
       o << "    sv += Grp<32>::other_d<1>(sv); bd += Grp<32>::other_d<1>(bd);\n";
       o << "    sv += Grp<32>::other_d<2>(sv); bd += Grp<32>::other_d<2>(bd);\n";
       o << "    lp += bd != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, sv);\n";
     } else {
-      o << "    double p[4];\n";
-      o << "#pragma unroll\n    for (int v = 0; v < 4; ++v) {\n      double acc = 0.0;\n";
+      o << "    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;\n";
+      o << "#pragma nounroll\n    for (int v = 0; v < 4; ++v) {\n      double acc = 0.0;\n";
       o << "      for (int i = 4 * r + v; i < " << N.len << "; i += 32) {\n";
       std::string a = "0.0", bb = "0.0", ct = "0.0";
       if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
       if (N.expr[1] >= 0) bb = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
       if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
       o << "        acc = acc + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
-        << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n      }\n      p[v] = acc;\n    }\n";
-      o << "    double sv = (p[0] + p[1]) + (p[2] + p[3]);\n";
+        << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n      }\n";
+      o << "      p0 = v == 0 ? acc : p0;\n      p1 = v == 1 ? acc : p1;\n      p2 = v == 2 ? acc : p2;\n      p3 = v == 3 ? acc : p3;\n    }\n";
+      o << "    double sv = (p0 + p1) + (p2 + p3);\n";
       o << "    sv += Grp<32>::other_d<0>(sv);\n    sv += Grp<32>::other_d<1>(sv);\n    sv += Grp<32>::other_d<2>(sv);\n";
       o << "    lp += sv;\n";
     }
@@ -272,7 +275,12 @@ bool read_file(const std::string& path, std::vector<char>& out) {
 std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir, unsigned kinds, int dmax) {
   std::ostringstream o;
   o << "// node-IR sweep kernel specialised for one model (generated by ir_jit.cpp)\n";
-  o << "#define MMB_IR_JIT 1\n#define MMB_IR_DMAX " << dmax << "\n#include \"device.h\"\n\n";
+  // occupancy target of the specialised kernel (MMB_IR_JIT_WAVES, default 4 waves per SIMD: the
+  // straight-line model code fits 128 VGPRs where the interpreter needed 2 waves' budget)
+  int waves = 4;
+  if (const char* w = std::getenv("MMB_IR_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(w)));
+  o << "#define MMB_IR_JIT 1\n#define MMB_IR_DMAX " << dmax << "\n#define MMB_IR_WAVES " << waves
+    << "\n#include \"device.h\"\n\n";
   // a uniform pool value (scalar load): data may change between models of the same structure,
   // so the source -- and the cached code object -- depends on the model's structure only
   o << "__device__ __forceinline__ double mmb_jit_uload(const double* p, int k) {\n"

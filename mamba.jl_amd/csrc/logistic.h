@@ -47,4 +47,10 @@ struct LgArgs {
                            //        requests one gradient per step)
   unsigned long long* ngrad;  // total gradient evaluations of the window
   unsigned long long* nstat;  // NUTS {updates, depth-cap hits, depth sum} (nuts.h Env::stat)
+  // gradient scheme: fd = 0 the analytic gradient (one column per request), fd = 1 Calculus
+  // forward differences (simulation.jl:47-51, the reference's default dtype=:forward): nv = p + 1
+  // logpdf! columns per request -- the position and each coordinate moved by its epsilon -- as
+  // virtual columns slot * nv + k of the gradient kernel (log-density partials only)
+  int32_t fd, nv;
+  int64_t Kv;              // column stride of the partial arrays: K (analytic) or K * nv (fd)
 };

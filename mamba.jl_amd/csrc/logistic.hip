@@ -120,6 +120,58 @@ __device__ __forceinline__ static void lg_assemble(const LgArgs& A, int slot, in
   S.lf = lf;
 }
 
+// logpdf!(m, x, block) and gradlogpdf!(m, x, block; dtype = :forward) at S.x (simulation.jl:47-51,
+// oracle logf_grad): Calculus forward differences over the request's nv = p + 1 columns (column 0
+// the position, column k its coordinate k - 1 moved by epsilon_{k-1} = 2^-26 max(1, |x|)), each
+// column's logpdf! = 0 + prior (the 64-lane butterfly of squares, d_iso) + the group sums of its
+// log-likelihood partials in group order when finite; lane e forms column e + 1 and the gradient
+// entry (f_{e+1} - f_0) / epsilon_e, non-finite -> 0 (sampler.jl:110).
+template <bool FOLD, class ST>
+__device__ __forceinline__ static void lg_assemble_fd(const LgArgs& A, int slot, int lane, const Grp<64>& g,
+                                                      ST& S) {
+  const int p = A.p;
+  const bool el = lane < p;
+  const double x = S.x[0];
+  const double ax = fabs(x);
+  const double eps = 0x1p-26 * (isnan(ax) ? ax : (ax > 1.0 ? ax : 1.0));
+  const double xp = x + eps;
+  const double sq = el ? 0.0 + x * x : 0.0;
+  const double sd = A.prior_sd;
+  double f0 = 0.0 + (__ballot(el && !isfinite(x)) ? -__builtin_inf() : d_iso(p, sd, g.sum(sq)));
+  double fk = 0.0;
+  for (int e = 0; e < p; ++e) {  // column e + 1's prior: lane e's square replaced
+    const double sqe = lane == e ? 0.0 + xp * xp : sq;
+    const bool bad = __ballot(el && !isfinite(lane == e ? xp : x)) != 0;
+    const double s = g.sum(sqe);
+    const double pr = 0.0 + (bad ? -__builtin_inf() : d_iso(p, sd, s));
+    fk = lane == e ? pr : fk;
+  }
+  constexpr int NW = FOLD ? 1 : MMB_LG_NS;  // partials read per group
+  const int64_t c0 = (int64_t)slot * A.nv, ck = c0 + lane + 1;
+  if (isfinite(f0)) {
+    double ylp = 0.0;
+    for (int r = 0; r < MMB_LG_NG; ++r) {
+      double ls = A.lpart[(size_t)(r * MMB_LG_NS) * A.Kv + c0];
+      for (int w = 1; w < NW; ++w) ls = ls + A.lpart[(size_t)(r * MMB_LG_NS + w) * A.Kv + c0];
+      ylp = ylp + ls;
+    }
+    f0 = f0 + ylp;
+  }
+  if (el && isfinite(fk)) {
+    double ylp = 0.0;
+    for (int r = 0; r < MMB_LG_NG; ++r) {
+      double ls = A.lpart[(size_t)(r * MMB_LG_NS) * A.Kv + ck];
+      for (int w = 1; w < NW; ++w) ls = ls + A.lpart[(size_t)(r * MMB_LG_NS + w) * A.Kv + ck];
+      ylp = ylp + ls;
+    }
+    fk = fk + ylp;
+  }
+  double gk = (fk - f0) / eps;
+  if (!isfinite(gk)) gk = 0.0;
+  S.g[0] = el ? gk : 0.0;
+  S.lf = f0;
+}
+
 // The per-chain sampler machine driven by lg_ctl_kernel: NUTS (nuts.h) or HMC/MALA (hmc.h).
 struct LgNuts {
   using St = NU::St;
@@ -226,8 +278,13 @@ __global__ __launch_bounds__(256, MMB_LG_CTL_WAVES) void lg_ctl_kernel(const LgA
   if (MC::wants(S.pc)) {
     // the chain's gradient slot is its index in the request list (slot assignment below)
     const int slot = start ? A.iv[(size_t)c * MMB_LG_NIV + 10] : si;
-    if (fold) lg_assemble<true>(A, slot, lane, g, S);
-    else lg_assemble<false>(A, slot, lane, g, S);
+    if (A.fd) {
+      if (fold) lg_assemble_fd<true>(A, slot, lane, g, S);
+      else lg_assemble_fd<false>(A, slot, lane, g, S);
+    } else {
+      if (fold) lg_assemble<true>(A, slot, lane, g, S);
+      else lg_assemble<false>(A, slot, lane, g, S);
+    }
   }
   const uint32_t chain = A.chain_offset + (uint32_t)c;
   for (;;) {
@@ -285,13 +342,17 @@ __global__ __launch_bounds__(256, MMB_LG_CTL_WAVES) void lg_ctl_kernel(const LgA
 // sub-ranges one after the other -- each its own fma chain from zero, as in the one-unit mode --
 // and writes the group's ((P0 + P1) + ..) to unit slot group * MMB_LG_NS: half the partials
 // written here and read by the control kernel, the same bits.
-template <int KS, bool FOLD>
+// LPONLY (forward differences): column v = request slot * nv + k is the request's position with
+// coordinate k - 1 moved by Calculus' epsilon (k = 0: unmoved), formed here from the position in
+// the same operation as the oracle (x + eps); only the log-density partials are written.
+template <int KS, bool FOLD, bool LPONLY>
 __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs A, int parity) {
   __shared__ __attribute__((aligned(16))) double xs[LG_RB][LG_LD];
   __shared__ double ys[LG_RB];
-  const int nact = A.count[parity];
+  const int nreq = A.count[parity];
+  const int nact = nreq * A.nv;  // columns
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (nact > 0) atomicAdd(A.ngrad, (unsigned long long)nact);
+    if (nreq > 0) atomicAdd(A.ngrad, (unsigned long long)nreq);
     A.count[parity ^ 1] = 0;  // the next control kernel's counter (its input list was read before)
   }
   const int b = (int)blockIdx.x;
@@ -308,8 +369,16 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
   const int slot = ct * 64 + w * 16 + lc;
   const bool live = slot < nact;
   double bpos[KS];
+  const int rs = LPONLY ? slot / A.nv : slot, kcol = LPONLY ? slot - rs * A.nv : 0;
 #pragma unroll
-  for (int kk = 0; kk < KS; ++kk) bpos[kk] = live ? A.pos[(size_t)slot * 64 + 4 * kk + lq] : 0.0;
+  for (int kk = 0; kk < KS; ++kk) {
+    double b = live ? A.pos[(size_t)rs * 64 + 4 * kk + lq] : 0.0;
+    if (LPONLY && 4 * kk + lq == kcol - 1) {  // oracle logf_grad: xx[k] = x[k] + eps
+      const double ax = fabs(b);
+      b = b + 0x1p-26 * (isnan(ax) ? ax : (ax > 1.0 ? ax : 1.0));
+    }
+    bpos[kk] = b;
+  }
   mmb_d4 tot[4], acc[4];
   double ltot = 0.0;
   const int rps = A.rps;
@@ -389,12 +458,14 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
         lprod = lprod * fac[h][i];
       }
       if (h == 1 && !two) break;
+      if constexpr (!LPONLY) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 * h + 4 * i + lq][16 * mt + lc], sres[h][i], acc[mt],
-                                                         0, 0, 0);
+          for (int mt = 0; mt < 4; ++mt)
+            acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[16 * h + 4 * i + lq][16 * mt + lc], sres[h][i],
+                                                           acc[mt], 0, 0, 0);
+      }
     }
     mmb_lg_renorm(&lprod, &lexp);  // < 2^9 before: never overflows
     if (ps == npass - 1) {  // end of a sub-range: its partials, folded into the group's in order
@@ -418,13 +489,15 @@ __global__ __launch_bounds__(256, MMB_LG_WAVES) void lg_grad_kernel(const LgArgs
     }
   }
   if (!live) return;
-  // coefficient 16 mt + lq + 4 q of chain lc
-  double* gp = A.gpart + ((size_t)un0 * A.K + slot) * 64;
+  if constexpr (!LPONLY) {
+    // coefficient 16 mt + lq + 4 q of chain lc
+    double* gp = A.gpart + ((size_t)un0 * A.K + slot) * 64;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) gp[16 * mt + lq + 4 * qq] = tot[mt][qq];
-  if (lq == 0) A.lpart[(size_t)un0 * A.K + slot] = ltot;
+      for (int qq = 0; qq < 4; ++qq) gp[16 * mt + lq + 4 * qq] = tot[mt][qq];
+  }
+  if (lq == 0) A.lpart[(size_t)un0 * A.Kv + slot] = ltot;
 }
 
 // nbound: an upper bound of the chains still running (the host's last read of the request
@@ -440,15 +513,22 @@ hipError_t mmb_lg_launch_ctl(const LgArgs& A, int start, int parity, int nbound,
     hipLaunchKernelGGL(lg_ctl_kernel<LgNuts>, grid, blk, 0, st, A, start, parity, fold);
   return hipGetLastError();
 }
-hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, int fold, hipStream_t st) {
-  const int tiles = (nbound + 63) / 64;
-  const dim3 grid((fold ? MMB_LG_NG : MMB_LG_NG * MMB_LG_NS) * tiles), blk(256);
+template <bool LPONLY>
+static void launch_grad(const LgArgs& A, int parity, int fold, dim3 grid, hipStream_t st) {
+  const dim3 blk(256);
   if (A.p <= 52) {
-    if (fold) hipLaunchKernelGGL((lg_grad_kernel<13, true>), grid, blk, 0, st, A, parity);
-    else hipLaunchKernelGGL((lg_grad_kernel<13, false>), grid, blk, 0, st, A, parity);
+    if (fold) hipLaunchKernelGGL((lg_grad_kernel<13, true, LPONLY>), grid, blk, 0, st, A, parity);
+    else hipLaunchKernelGGL((lg_grad_kernel<13, false, LPONLY>), grid, blk, 0, st, A, parity);
   } else {
-    if (fold) hipLaunchKernelGGL((lg_grad_kernel<16, true>), grid, blk, 0, st, A, parity);
-    else hipLaunchKernelGGL((lg_grad_kernel<16, false>), grid, blk, 0, st, A, parity);
+    if (fold) hipLaunchKernelGGL((lg_grad_kernel<16, true, LPONLY>), grid, blk, 0, st, A, parity);
+    else hipLaunchKernelGGL((lg_grad_kernel<16, false, LPONLY>), grid, blk, 0, st, A, parity);
   }
+}
+// nbound: requests (chains); the grid covers their nbound * nv columns
+hipError_t mmb_lg_launch_grad(const LgArgs& A, int parity, int nbound, int fold, hipStream_t st) {
+  const int tiles = (int)(((int64_t)nbound * A.nv + 63) / 64);
+  const dim3 grid((fold ? MMB_LG_NG : MMB_LG_NG * MMB_LG_NS) * tiles);
+  if (A.fd) launch_grad<true>(A, parity, fold, grid, st);
+  else launch_grad<false>(A, parity, fold, grid, st);
   return hipGetLastError();
 }

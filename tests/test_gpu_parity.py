@@ -594,6 +594,44 @@ def test_logistic_nuts_parity_full(mamba, oracle):
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
 
 
+@pytest.mark.parametrize("sampler", ["nuts", "hmc", "mala"])
+def test_logistic_forward_difference_parity(mamba, oracle, sampler):
+    """The reference's default gradient on config 4's model: NUTS("beta") with no dtype is
+    gradlogpdf!(...; dtype = :forward) (nuts.jl:47-56 -> simulation.jl:47-51, Calculus forward
+    differences), run as p + 1 log-density columns per request through the batched MFMA kernel
+    (logistic.hip lg_grad_kernel<.., LPONLY>, lg_assemble_fd).  Bit-exact against the oracle's
+    restatement (oracle.c logf_grad: logf at x and at x + eps_k e_k in the same summation spec)."""
+    sch = {"nuts": [mamba.NUTS("beta")], "hmc": [mamba.HMC("beta", 0.01, 3)], "mala": [mamba.MALA("beta", 2e-4)]}
+    m, _ = logistic(mamba, 1000, 50, sch[sampler])
+    assert m.samplers[0].gradient == mamba.abi.MMB_GRAD_FORWARD
+    K = 70
+    init = np.random.default_rng(41).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 12, 2, 1, model_burnin=6)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+    assert np.abs(dg[-1] - dg[0]).max() > 0
+
+
+def test_logistic_forward_difference_full_size(mamba, oracle):
+    """Forward differences at config 4's size (N = 10000, p = 50): 51 columns per request, group
+    mode (>= 1024 columns), the 160-row sub-ranges; K = 70 NUTS chains, bit-exact vs the oracle,
+    and the gradient within forward-difference error of the analytic one."""
+    m, _ = logistic(mamba, 10000, 50, [mamba.NUTS("beta")])
+    K = 70
+    init = np.random.default_rng(42).normal(0.0, 0.1, (K, 50))
+    eng, dg, st, do = both(mamba, oracle, m, init, 4, 1, 1, model_burnin=2)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+    # the two gradients of one position agree to forward-difference accuracy
+    x = st["values"][0]
+    _, gf = oracle.block_logpdf(m, st["values"][0], 0, x, grad=True)
+    ma, _ = logistic(mamba, 10000, 50, [mamba.NUTS("beta", dtype="analytic")])
+    _, ga = oracle.block_logpdf(ma, st["values"][0], 0, x, grad=True)
+    np.testing.assert_allclose(gf, ga, rtol=0, atol=1e-4 * np.abs(ga).max() + 1e-3)
+
+
 @pytest.mark.parametrize("p", [53, 64])
 def test_logistic_wide_parity(mamba, oracle, p):
     """53 <= p <= MMB_LG_DV: the 16-k-step first GEMM (coefficients 52..63 are part of eta)."""
@@ -757,16 +795,13 @@ def test_rats_scale_total_on_one_gpu(mamba, oracle):
 
 
 def test_gradient_choice_validated(mamba):
-    """mmb_gradient (include/mamba_hip.h): forward differences are not available on the logistic
-    kernel, the analytic gradient not on the node IR; both are refused at mmb_create.  The
-    reference's default NUTS(:beta) (dtype=:forward) on logistic is refused, never silently
-    given the analytic gradient."""
+    """mmb_gradient (include/mamba_hip.h): the analytic gradient is not available on the node IR
+    and is refused at mmb_create; the reference's default NUTS(:beta) (dtype=:forward) on
+    logistic now runs its forward differences on the device (test_logistic_forward_difference_*)."""
     A = mamba.abi
     m = mamba.logistic(200, 5, 10.0)
     m.setsamplers([mamba.NUTS("beta")])
     assert m.samplers[0].gradient == A.MMB_GRAD_FORWARD
-    with pytest.raises(RuntimeError, match="forward-difference"):
-        mamba.Engine(m)
     ir = mamba.ir
     mi = ir.seeds_model().setinputs(ir.SEEDS)
     mi.setsamplers([mamba.NUTS(["alpha0", "alpha1", "alpha2", "alpha12"], dtype="analytic"), mamba.AMWG("b", 0.01),
