@@ -7,7 +7,7 @@ mu_beta, Gibbs s2_beta; AMM adapt=:all so every update runs the 30x30 pivoted
 Cholesky), 16384 chains per GPU (weak scaling; N GPUs = N*16384 chains, configs[4] at
 N=8).  A step = one sample!(m) sweep of every chain (one mcmc_worker! iteration) incl.
 the keep rule and the Chains write (thin 2, draws kept in HBM).  Steps run as one
-mmb_run window (kernels of 8 iterations); state and data are resident in HBM.
+mmb_run window (kernels of up to 20 iterations, equal launches); state and data are resident in HBM.
 
 Steady state: before --warmup, an untimed adaptation pre-run (--adapt-prerun, default
 128 >= 2d+2 = 62 for the 30-d AMM blocks) takes every chain past AMM's switch to the
@@ -476,8 +476,8 @@ def main():
                 "gradients_per_chain_update_timed": grads_timed / (K * args.steps),
                 "window": f"timed run: {args.steps} iterations, burnin {tburn}"}
     else:
-        W = int(os.environ.get("MMB_ITERS_PER_LAUNCH",
-                               "16" if args.workload == "rats" or args.workload.endswith("_ir") else "256"))
+        W = int(os.environ.get("MMB_ITERS_PER_LAUNCH", "20" if args.workload == "rats" else
+                               "16" if args.workload.endswith("_ir") else "256"))
         # the timed window's own launches, HIP events on the engine stream (measured before the
         # collective: a separate window after it started on a GPU clocked down during the RCCL
         # init's idle seconds and read ~10 % slow)
@@ -540,7 +540,7 @@ def main():
     if nuts:
         out["config"]["gradient"] = args.gradient
     if args.workload == "rats":
-        out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "16")),
+        out["config"].update({"iters_per_launch": int(os.environ.get("MMB_ITERS_PER_LAUNCH", "20")),
                               "scheme": args.scheme})
         if args.scheme == "gibbs_amm":
             out["config"]["amm_adapt"] = "all"

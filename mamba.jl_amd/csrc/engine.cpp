@@ -1146,10 +1146,11 @@ static void fill_args(const mmb_engine* e, SweepArgs& A) {
 static int iters_per_launch(const mmb_engine* e) {
   const char* s = std::getenv("MMB_ITERS_PER_LAUNCH");
   if (s && std::atoi(s) > 0) return std::atoi(s);
-  // rats: 16 (16384 chains: 2.2 ms launches, 0.5-0.9 % over 8 and 6 % over 4 in the round-4 A/B,
-  // the launch tail amortised); line: 256 (an iteration of the quad kernel is ~8 us, so 64 per
-  // launch left a launch gap every ~0.5 ms)
-  return e->model == MMB_MODEL_RATS ? 16 : e->model == MMB_MODEL_IR ? 16 : e->model == MMB_MODEL_LINE ? 256 : 64;
+  // rats: 20 (16384 chains: ~2.5 ms launches; 16 was 0.5-0.9 % over 8 and 6 % over 4 in the
+  // round-4 A/B, the launch tail amortised; round 5: 20 as fast as 16 and 32 over 400 steps, and a
+  // 20-iteration window runs as one launch: 1.226e8 vs 1.21e8 for 10 + 10); line: 256 (an
+  // iteration of the quad kernel is ~8 us, so 64 per launch left a launch gap every ~0.5 ms)
+  return e->model == MMB_MODEL_RATS ? 20 : e->model == MMB_MODEL_IR ? 16 : e->model == MMB_MODEL_LINE ? 256 : 64;
 }
 
 template <class T>
