@@ -54,13 +54,19 @@ __device__ __forceinline__ double qbc(double x) {
   return mmb_u2d((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32));
 }
 
-// factor entry L[slot(e, q)] of the register copy (d <= 3: slots 0..5), q a run-time index
+// factor entry L[slot(e, q)] of the register copy (d <= 3: slots 0..5), q a run-time index.
+// Bitwise blends, not selects: a chain of `t == u ? L[u] : r` was turned back into an indexed
+// array, placed in LDS by the compiler, with a load and a full lgkmcnt wait per entry read.
 __device__ __forceinline__ double lsel(const double (&L)[6], int e, int q) {
   const int t = mmb_slot(e, q);
-  double r = L[0];
+  uint64_t r = 0;
 #pragma unroll
-  for (int u = 1; u < 6; ++u) r = t == u ? L[u] : r;
-  return r;
+  for (int u = 0; u < 6; ++u) {
+    uint64_t msk = (uint64_t)0 - (uint64_t)(t == u);
+    asm volatile("" : "+v"(msk));
+    r |= mmb_d2u(L[u]) & msk;
+  }
+  return mmb_u2d(r);
 }
 __device__ __forceinline__ double zsel(const double (&z)[3], int k) {
   return k == 0 ? z[0] : k == 1 ? z[1] : z[2];
@@ -308,12 +314,23 @@ __device__ __forceinline__ void line_draw(const SweepArgs& A, uint32_t chain, in
 }
 }  // namespace
 
-__global__ __launch_bounds__(64) void line_amm_kernel(const SweepArgs A) {
+__global__ __launch_bounds__(64) void line_amm_kernel(const SweepArgs Ak) {
   const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) / LQ);
-  if (c >= A.K) return;  // whole quads exit together
+  if (c >= Ak.K) return;  // whole quads exit together
   const int lane = (int)(threadIdx.x & (LQ - 1));
   const Grp<1> g1;  // the replicated (one-lane) arithmetic of Mdl<LINE>
-  const DBlock& B = mmb_block(A.blocks, 0);
+  // the descriptor and the arguments the update loop reads, copied once into registers: read
+  // through their constant-memory references, the compiler re-issued scalar loads of them inside
+  // the loop under SGPR pressure, each followed by a full lgkmcnt wait (18 per iteration)
+  DBlock B = mmb_block(Ak.blocks, 0);
+  SweepArgs A = Ak;
+  asm volatile("" : "+v"(B.adapt), "+v"(B.sigl_diag), "+v"(B.transform), "+v"(B.nn), "+v"(B.d));
+  asm volatile("" : "+v"(B.nodes[0]), "+v"(B.nodes[1]), "+v"(B.nodes[2]), "+v"(B.emap[0]), "+v"(B.emap[1]),
+               "+v"(B.emap[2]));
+  asm volatile("" : "+v"(B.beta), "+v"(B.scale), "+v"(A.ig_c), "+v"(A.burnin), "+v"(A.thin),
+               "+v"(A.model_burnin), "+v"(A.kept_origin));
+#pragma unroll
+  for (int i = 0; i < 5; ++i) asm volatile("" : "+v"(A.lx[i]), "+v"(A.ly[i]));
   const int d = B.d;
   const int T = mmb_tri(d);
   const uint32_t chain = A.chain_offset + (uint32_t)c;
