@@ -387,7 +387,13 @@ def main():
     value = total_units / dt
     ms_per_step = dt / args.steps * 1e3
     kernel_ms_per_step = t_kms / args.steps
-    if kernel_ms_per_step > 1.05 * ms_per_step:
+    # logistic: the window's chains run as independent parts on their own streams (engine.cpp
+    # run_logistic), so the summed gradient-kernel time may exceed the wall time up to that factor
+    lg_parts = 1
+    if nuts:
+        lg_parts = max(1, min(4, int(os.environ.get("MMB_LG_SPLIT", "3"))))
+        lg_parts = 1 if K < 32 * lg_parts else lg_parts
+    if kernel_ms_per_step > 1.05 * ms_per_step * lg_parts:
         raise SystemExit(f"bench: kernel time per step {kernel_ms_per_step:.4f} ms exceeds the timed "
                          f"window's {ms_per_step:.4f} ms by more than 5 % — timing is inconsistent")
     grads_timed = eng.grad_evals() if nuts else 0  # (the counter restarts with every mmb_run)
@@ -464,14 +470,15 @@ def main():
         per_grad = 4.0 * 10000 * 50 if args.gradient == "analytic" else 2.0 * 10000 * 50 * 51
         flops = per_grad * grads_timed
         achieved = flops / (kms * 1e-3) / 1e12
-        # the same flops over the window's wall time: the gradient launches are 77 % of it, the
-        # control kernel (NUTS machines, partial folding) 22 %, launch gaps 0.5 % (rocprofv3 trace,
-        # profiles/r4_logistic_walltime_split.json)
+        # the same flops over the window's wall time (one stream: the gradient launches were 77 %
+        # of it, the control kernel 22 %, launch gaps 0.5 %, profiles/r4_logistic_walltime_split.json;
+        # with the chains split over streams the parts' kernels overlap, and the per-launch
+        # durations include that sharing)
         wall_tfs = flops / dt / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None,
                 "achieved_wall": wall_tfs, "frac_wall": wall_tfs / F64_MFMA_PEAK_TFS,
-                "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": per_grad,
+                "kernel": "lg_grad_kernel", "algorithmic_flops_per_gradient": per_grad, "streams": lg_parts,
                 "avg_launch_ms": kms / launches, "gradients_per_launch": grads_timed / launches,
                 "gradients_per_chain_update_timed": grads_timed / (K * args.steps),
                 "window": f"timed run: {args.steps} iterations, burnin {tburn}"}

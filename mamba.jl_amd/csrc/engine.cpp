@@ -87,7 +87,10 @@ struct mmb_engine {
   double *lg_gpart = nullptr, *lg_lpart = nullptr;
   int32_t *lg_iv = nullptr, *lg_count = nullptr, *lg_hcount = nullptr, *lg_s2c = nullptr;
   int64_t* lg_itc = nullptr;
-  hipEvent_t lg_cev[2] = {nullptr, nullptr};  // request-count readbacks in flight (run_logistic)
+  hipEvent_t lg_cev[2 * MMB_LG_SPLIT_MAX] = {};  // request-count readbacks in flight, 2 per part (run_logistic)
+  hipStream_t lg_streamx[MMB_LG_SPLIT_MAX - 1] = {};   // the streams of parts 1.. (part 0: the engine stream)
+  hipEvent_t lg_join[MMB_LG_SPLIT_MAX] = {};          // fork / join of the streams
+  std::vector<hipEvent_t> evpoolx[MMB_LG_SPLIT_MAX - 1];  // kernel timing events of parts 1..
   int64_t lg_steps = 0;  // gradient steps of the last window
   unsigned long long* lg_ngrad = nullptr;
   int32_t* d_cperm = nullptr;  // lane-group slot -> chain of the 32-lane sweep kernels (order_chains)
@@ -817,6 +820,12 @@ void mmb_destroy(mmb_engine* e) {
   if (e->lg_hcount) (void)hipHostFree(e->lg_hcount);
   for (hipEvent_t ev : e->lg_cev)
     if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->lg_join)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto& pool : e->evpoolx)
+    for (hipEvent_t ev : pool) (void)hipEventDestroy(ev);
+  for (hipStream_t q : e->lg_streamx)
+    if (q) (void)hipStreamDestroy(q);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   for (hipEvent_t ev : e->evpool) (void)hipEventDestroy(ev);
@@ -1086,12 +1095,16 @@ int mmb_init_chains(mmb_engine* e, const double* init, int64_t K, int64_t chain_
     HIPCHK(e, dalloc(&e->lg_pos, (size_t)K * MMB_LG_DV));
     HIPCHK(e, dalloc(&e->lg_gpart, (size_t)MMB_LG_NG * MMB_LG_NS * K * MMB_LG_DV));
     HIPCHK(e, dalloc(&e->lg_lpart, (size_t)MMB_LG_NG * MMB_LG_NS * K * (e->lg_fd ? e->lg_p + 1 : 1)));
-    HIPCHK(e, dalloc(&e->lg_count, 2));
+    HIPCHK(e, dalloc(&e->lg_count, 2 * MMB_LG_SPLIT_MAX));
     HIPCHK(e, dalloc(&e->lg_s2c, (size_t)2 * K));
     HIPCHK(e, dalloc(&e->lg_ngrad, 1));
-    if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, 2 * sizeof(int32_t), 0));
+    if (!e->lg_hcount) HIPCHK(e, hipHostMalloc(&e->lg_hcount, 2 * MMB_LG_SPLIT_MAX * sizeof(int32_t), 0));
     for (hipEvent_t& ev : e->lg_cev)
       if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (hipEvent_t& ev : e->lg_join)
+      if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (hipStream_t& q : e->lg_streamx)
+      if (!q) HIPCHK(e, hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   }
   int rc = upload_blocks(e);
   if (rc) return rc;
@@ -1217,7 +1230,15 @@ static int launch_width(int64_t iters, int W, int64_t li) {
 
 // Config-4 window: ctl / grad kernel pairs until no chain requests a gradient.  The
 // request count is read back every LG_CHECK steps (pinned host words, one check behind the
-// launches); surplus pairs after the last chain finished are no-ops (the grad kernel exits on count 0, idle chains return).
+// launches); surplus pairs after the last chain finished are no-ops (the grad kernel exits on
+// count 0, idle chains return).
+//
+// The chains run as independent parts (default 3, MMB_LG_SPLIT=1..4), each on its own stream
+// with its own request list, partial buffers and count words: a step is a latency-bound control
+// kernel (one wave per chain, little arithmetic) behind an MFMA gradient kernel, and the other
+// part's gradient kernel fills the GPU while one part is in its control kernel (and the window's
+// tail, where few chains still run, overlaps across the parts).  Every chain keeps its own state,
+// Philox id and draws column, so the draws are identical for any split.
 #ifndef MMB_LG_FOLD_MIN
 #define MMB_LG_FOLD_MIN 1024  // chains: 16 tiles x 32 groups = 512 workgroups
 #endif
@@ -1225,30 +1246,65 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
                         bool want) {
   constexpr int LG_CHECK = 8;
   const BlockHost& h = e->blocks[0];
-  LgArgs A;
-  std::memset(&A, 0, sizeof A);
-  A.K = (int32_t)e->K; A.p = e->lg_p; A.N = e->lg_N; A.rps = e->lg_rps;
-  A.Np = MMB_LG_NG * MMB_LG_NS * e->lg_rps;
-  A.chain_offset = (uint32_t)e->chain_offset;
-  A.seed = e->seed;
-  A.iter0 = e->iter;
-  A.it_end = e->iter + a->iters;
-  A.burnin = a->burnin; A.thin = a->thin; A.model_burnin = a->model_burnin; A.kept_origin = kept0;
-  A.prior_sd = e->spec.prior_sd;
-  A.target = h.spec.target;
-  A.X = e->lg_X; A.y = e->lg_y;
-  A.vals = e->d_vals; A.vec = e->lg_vec; A.sc = e->lg_sc; A.iv = e->lg_iv; A.itc = e->lg_itc;
-  A.kind = h.spec.sampler;
-  A.frames = e->lg_frames; A.tm = h.m; A.tflags = h.flags;
-  A.tune = A.kind == MMB_SAMPLER_NUTS ? h.nuts : h.hmc;
-  A.sigl = h.sigl_d;
-  A.draws = draws;
-  A.pos = e->lg_pos; A.gpart = e->lg_gpart; A.lpart = e->lg_lpart; A.count = e->lg_count; A.s2c = e->lg_s2c;
-  A.ngrad = e->lg_ngrad;
-  A.nstat = e->d_nstat;
-  A.fd = e->lg_fd ? 1 : 0;
-  A.nv = e->lg_fd ? e->lg_p + 1 : 1;
-  A.Kv = e->K * A.nv;
+  LgArgs A0;
+  std::memset(&A0, 0, sizeof A0);
+  A0.K = (int32_t)e->K; A0.p = e->lg_p; A0.N = e->lg_N; A0.rps = e->lg_rps;
+  A0.Np = MMB_LG_NG * MMB_LG_NS * e->lg_rps;
+  A0.chain_offset = (uint32_t)e->chain_offset;
+  A0.seed = e->seed;
+  A0.iter0 = e->iter;
+  A0.it_end = e->iter + a->iters;
+  A0.burnin = a->burnin; A0.thin = a->thin; A0.model_burnin = a->model_burnin; A0.kept_origin = kept0;
+  A0.prior_sd = e->spec.prior_sd;
+  A0.target = h.spec.target;
+  A0.X = e->lg_X; A0.y = e->lg_y;
+  A0.vals = e->d_vals; A0.vec = e->lg_vec; A0.sc = e->lg_sc; A0.iv = e->lg_iv; A0.itc = e->lg_itc;
+  A0.kind = h.spec.sampler;
+  A0.frames = e->lg_frames; A0.tm = h.m; A0.tflags = h.flags;
+  A0.tune = A0.kind == MMB_SAMPLER_NUTS ? h.nuts : h.hmc;
+  const int tune_w = A0.kind == MMB_SAMPLER_NUTS ? 8 : 2;
+  A0.sigl = h.sigl_d;
+  A0.draws = draws;
+  A0.Kd = (int32_t)e->K;
+  A0.pos = e->lg_pos; A0.gpart = e->lg_gpart; A0.lpart = e->lg_lpart; A0.count = e->lg_count; A0.s2c = e->lg_s2c;
+  A0.ngrad = e->lg_ngrad;
+  A0.nstat = e->d_nstat;
+  A0.fd = e->lg_fd ? 1 : 0;
+  A0.nv = e->lg_fd ? e->lg_p + 1 : 1;
+  // default 3 parts: 1.34e6 chain-updates/s on config 4 vs 1.28e6 (2), 1.11e6 (4), 1.12e6 (1)
+  int nh = 3;
+  if (const char* hs = std::getenv("MMB_LG_SPLIT")) nh = std::max(1, std::min(MMB_LG_SPLIT_MAX, std::atoi(hs)));
+  if (e->K < 32 * nh) nh = 1;
+  struct Half {
+    LgArgs A;
+    hipStream_t st;
+    std::vector<hipEvent_t>* ev;
+    int64_t s = 0;
+    int nbound = 0;
+    bool done = false;
+  } H[MMB_LG_SPLIT_MAX];
+  for (int i = 0; i < nh; ++i) {
+    // chains [b, b + k) of the engine: every per-chain array offset by b rows, the partial and
+    // request buffers split in proportion (each half indexes them with its own K)
+    const int64_t b = e->K * i / nh, k = e->K * (i + 1) / nh - b;
+    LgArgs& A = H[i].A;
+    A = A0;
+    A.K = (int32_t)k;
+    A.Kv = k * A.nv;
+    A.chain_offset = (uint32_t)(e->chain_offset + b);
+    A.vals += b * MMB_LG_DV; A.vec += b * MMB_LG_NVEC * MMB_LG_DV; A.sc += b * MMB_LG_NSC;
+    A.iv += b * MMB_LG_NIV; A.itc += b; A.frames += b * NutsFrames<MMB_LG_DV>::DBL;
+    A.tune += b * tune_w; A.tm += b; A.tflags += b;
+    if (A.draws) A.draws += b;
+    A.pos += b * MMB_LG_DV;
+    A.gpart += (size_t)MMB_LG_NG * MMB_LG_NS * b * MMB_LG_DV;
+    A.lpart += (size_t)MMB_LG_NG * MMB_LG_NS * b * A.nv;
+    A.count += 2 * i;
+    A.s2c += 2 * b;
+    H[i].st = i == 0 ? e->stream : e->lg_streamx[i - 1];
+    H[i].ev = i == 0 ? &e->evpool : &e->evpoolx[i - 1];
+    H[i].nbound = (int)k;
+  }
   HIPCHK(e, hipMemsetAsync(e->lg_ngrad, 0, sizeof(unsigned long long), e->stream));
   e->kernel_ms = 0.0;
   e->launches = 0;
@@ -1258,67 +1314,92 @@ static int run_logistic(mmb_engine* e, const mmb_run_args* a, double* draws, int
     // every update needs >= 1 gradient; a NUTS tree has <= 2^depth leaves and nutsepsilon
     // <= 4001; HMC needs L + 1 gradients per update, MALA 2
     int64_t per = (1LL << MMB_NUTS_MAX_DEPTH) + 2, extra = 4002;
-    if (A.kind != MMB_SAMPLER_NUTS) {
+    if (A0.kind != MMB_SAMPLER_NUTS) {
       std::vector<double> th;
       int rc = d2h(e, th, h.hmc, e->K * 2);
       if (rc) return rc;
       double lmax = 0.0;
       for (int64_t k = 0; k < e->K; ++k) lmax = std::max(lmax, th[k * 2 + 1]);
-      per = A.kind == MMB_SAMPLER_MALA ? 2 : (int64_t)std::max(lmax, 0.0) + 1;
+      per = A0.kind == MMB_SAMPLER_MALA ? 2 : (int64_t)std::max(lmax, 0.0) + 1;
       extra = 0;
     }
     const int64_t cap = a->iters * per + extra + 4 * LG_CHECK;
-    std::vector<hipEvent_t>& ev = e->evpool;
-    HIPCHK(e, hipMemsetAsync(e->lg_count, 0, 2 * sizeof(int32_t), e->stream));
-    hipError_t st = mmb_lg_launch_ctl(A, 1, 0, (int)e->K, 0, e->stream);
-    if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
-    int64_t s = 0;
-    int nbound = (int)e->K;  // running chains, as last read back (non-increasing in a window)
-    for (;;) {
-      const int par = (int)(s & 1);
-      if (a->time_kernels) {
-        while ((int64_t)ev.size() < 2 * (s + 1)) {
-          hipEvent_t x;
-          HIPCHK(e, hipEventCreate(&x));
-          ev.push_back(x);
-        }
-        HIPCHK(e, hipEventRecord(ev[2 * s], e->stream));
-      }
-      // group mode once the step is wide enough to fill the GPU with one workgroup per
-      // (group, 64-chain tile): half the partial traffic; one workgroup per sub-range below
-      // that, where a step's latency is what counts
-      const int fold = (int64_t)nbound * A.nv >= MMB_LG_FOLD_MIN ? 1 : 0;
-      st = mmb_lg_launch_grad(A, par, nbound, fold, e->stream);
-      if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_grad launch: %s", hipGetErrorString(st));
-      if (a->time_kernels) HIPCHK(e, hipEventRecord(ev[2 * s + 1], e->stream));
-      st = mmb_lg_launch_ctl(A, 0, par ^ 1, nbound, fold, e->stream);
+    HIPCHK(e, hipMemsetAsync(e->lg_count, 0, 2 * MMB_LG_SPLIT_MAX * sizeof(int32_t), e->stream));
+    if (nh > 1) {  // fork: the part streams start behind everything queued on the engine stream
+      HIPCHK(e, hipEventRecord(e->lg_join[0], e->stream));
+      for (int i = 1; i < nh; ++i) HIPCHK(e, hipStreamWaitEvent(H[i].st, e->lg_join[0], 0));
+    }
+    for (int i = 0; i < nh; ++i) {
+      hipError_t st = mmb_lg_launch_ctl(H[i].A, 1, 0, H[i].A.K, 0, H[i].st);
       if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
-      ++s;
-      if (s % LG_CHECK == 0) {
-        // two readbacks in flight: wait for the one issued LG_CHECK steps ago, so the
-        // stream still holds LG_CHECK queued steps while the host decides (the count is
-        // non-increasing, so the older value is still a bound on the running chains)
-        const int j = (int)((s / LG_CHECK) & 1);
-        HIPCHK(e, hipMemcpyAsync(e->lg_hcount + j, e->lg_count + (s & 1), sizeof(int32_t),
-                                 hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipEventRecord(e->lg_cev[j], e->stream));
-        const int jw = s >= 2 * LG_CHECK ? j ^ 1 : j;  // the first check waits for its own copy
-        HIPCHK(e, hipEventSynchronize(e->lg_cev[jw]));     // (short windows end without surplus)
-        if (e->lg_hcount[jw] == 0) break;
-        nbound = e->lg_hcount[jw];
-      }
-      if (s > cap) return fail(e, MMB_E_STATE, "logistic window did not terminate");
     }
-    e->lg_steps = s;
+    for (int live = nh; live > 0;) {
+      for (int i = 0; i < nh; ++i) {
+        Half& q = H[i];
+        if (q.done) continue;
+        const LgArgs& A = q.A;
+        const int64_t s = q.s;
+        const int par = (int)(s & 1);
+        std::vector<hipEvent_t>& ev = *q.ev;
+        if (a->time_kernels) {
+          while ((int64_t)ev.size() < 2 * (s + 1)) {
+            hipEvent_t x;
+            HIPCHK(e, hipEventCreate(&x));
+            ev.push_back(x);
+          }
+          HIPCHK(e, hipEventRecord(ev[2 * s], q.st));
+        }
+        // group mode once the step is wide enough to fill the GPU with one workgroup per
+        // (group, 64-chain tile): half the partial traffic; one workgroup per sub-range below
+        // that, where a step's latency is what counts
+        const int fold = (int64_t)q.nbound * A.nv * nh >= MMB_LG_FOLD_MIN ? 1 : 0;
+        hipError_t st = mmb_lg_launch_grad(A, par, q.nbound, fold, q.st);
+        if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_grad launch: %s", hipGetErrorString(st));
+        if (a->time_kernels) HIPCHK(e, hipEventRecord(ev[2 * s + 1], q.st));
+        st = mmb_lg_launch_ctl(A, 0, par ^ 1, q.nbound, fold, q.st);
+        if (st != hipSuccess) return fail(e, MMB_E_HIP, "lg_ctl launch: %s", hipGetErrorString(st));
+        q.s = s + 1;
+        if (q.s % LG_CHECK == 0) {
+          // two readbacks in flight: wait for the one issued LG_CHECK steps ago, so the
+          // stream still holds LG_CHECK queued steps while the host decides (the count is
+          // non-increasing, so the older value is still a bound on the running chains)
+          const int j = (int)((q.s / LG_CHECK) & 1);
+          int32_t* hc = e->lg_hcount + 2 * i;
+          hipEvent_t* cev = e->lg_cev + 2 * i;
+          HIPCHK(e, hipMemcpyAsync(hc + j, A.count + (q.s & 1), sizeof(int32_t), hipMemcpyDeviceToHost, q.st));
+          HIPCHK(e, hipEventRecord(cev[j], q.st));
+          const int jw = q.s >= 2 * LG_CHECK ? j ^ 1 : j;  // the first check waits for its own copy
+          HIPCHK(e, hipEventSynchronize(cev[jw]));         // (short windows end without surplus)
+          if (hc[jw] == 0) {
+            q.done = true;
+            --live;
+          } else {
+            q.nbound = hc[jw];
+          }
+        }
+        if (q.s > cap) return fail(e, MMB_E_STATE, "logistic window did not terminate");
+      }
+    }
+    for (int i = 1; i < nh; ++i) {  // join: later work on the engine stream sees every part's results
+      HIPCHK(e, hipEventRecord(e->lg_join[i], H[i].st));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->lg_join[i], 0));
+    }
+    int64_t steps = 0;
+    for (int i = 0; i < nh; ++i) steps = std::max(steps, H[i].s);
+    e->lg_steps = steps;
     if (a->time_kernels) {
-      HIPCHK(e, hipStreamSynchronize(e->stream));
-      for (int64_t i = 0; i < s; ++i) {
-        float ms = 0.f;
-        HIPCHK(e, hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
-        e->kernel_ms += ms;
+      // summed gradient-kernel durations of all parts (they may overlap in time)
+      for (int i = 0; i < nh; ++i) {
+        HIPCHK(e, hipStreamSynchronize(H[i].st));
+        for (int64_t t = 0; t < H[i].s; ++t) {
+          float ms = 0.f;
+          HIPCHK(e, hipEventElapsedTime(&ms, (*H[i].ev)[2 * t], (*H[i].ev)[2 * t + 1]));
+          e->kernel_ms += ms;
+        }
       }
     }
-    e->launches = s;
+    e->launches = 0;
+    for (int i = 0; i < nh; ++i) e->launches += H[i].s;
     e->units = a->iters * e->K;
   }
   e->iter += a->iters;

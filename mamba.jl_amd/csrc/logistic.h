@@ -14,6 +14,7 @@
 #define MMB_LG_NVEC 12  // machine vectors kept per chain besides v (nuts.h NutsM order)
 #define MMB_LG_NSC 16
 #define MMB_LG_NIV 16
+#define MMB_LG_SPLIT_MAX 4  // independent chain parts of a window, one stream each (engine.cpp run_logistic)
 
 struct LgArgs {
   int32_t kind;            // mmb_sampler_kind of the single block: NUTS, HMC or MALA
@@ -36,7 +37,9 @@ struct LgArgs {
   const double* sigl;      // HMC/MALA chol(Sigma) lower row-major p x p, or null (I)
   int32_t* tm;             // [K] m
   int32_t* tflags;         // [K]
-  double* draws;           // [n_kept][p][K] or null
+  double* draws;           // [n_kept][p][Kd] or null (this launch's chains from column 0)
+  int32_t Kd;              // draws column stride: the engine's chains (a window may run its chains
+                           // as independent halves, engine.cpp run_logistic)
   // gradient exchange between the two kernels
   double* pos;             // [K][64] positions of the chains that requested a gradient (slot order)
   double* gpart;           // [MMB_LG_NG * MMB_LG_NS][K][64] sub-range partials (one workgroup each)

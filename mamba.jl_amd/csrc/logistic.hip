@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256, MMB_LG_CTL_WAVES) void lg_ctl_kernel(const LgA
     itc = cur;  // mcmc_worker! keep rule (mcmc.jl:76): sim[i,:,1] = unlist(m, true)
     if (A.draws && itc > A.burnin && (itc - A.burnin) % A.thin == 0 && lane < A.p) {
       const int64_t row = (itc - A.burnin) / A.thin - 1 - A.kept_origin;
-      A.draws[(size_t)(row * A.p + lane) * A.K + c] = S.v[0];
+      A.draws[(size_t)(row * A.p + lane) * A.Kd + c] = S.v[0];
     }
     if (itc >= A.it_end) {
       S.pc = MC::IDLE;

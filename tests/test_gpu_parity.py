@@ -401,6 +401,27 @@ def test_logistic_nuts_parity(mamba, oracle):
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
 
 
+@pytest.mark.parametrize("grad", ["analytic", "forward"])
+def test_logistic_split_identical(mamba, monkeypatch, grad):
+    """A window runs its chains as independent parts on their own streams (engine.cpp
+    run_logistic): draws, state, tuning and gradient counts identical to one stream for 2 and 3
+    parts (unequal), at a width where the group-mode (fold) gradient kernel runs."""
+    m, _ = logistic(mamba, 1000, 50, [mamba.NUTS("beta", dtype=grad)])
+    K = 1500 if grad == "analytic" else 301
+    init = np.random.default_rng(21).normal(0.0, 0.1, (K, 50))
+    out = []
+    for split in ("1", "2", "3"):
+        monkeypatch.setenv("MMB_LG_SPLIT", split)
+        eng = mamba.Engine(m)
+        eng.init_chains(init, seed=5)
+        d = eng.run(12, burnin=0, thin=1, model_burnin=6)
+        out.append((d, eng.values(), eng.tune(), eng.grad_evals()))
+        eng.close()
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_logistic_device_gelman_rubin_matches_host(mamba):
     """p = 50 monitored values: the workgroup-per-chain-chunk Gelman-Rubin kernel."""
     m, _ = logistic(mamba, 1000, 50)
