@@ -201,7 +201,13 @@ struct Mdl<MMB_MODEL_IR> {
     put(B, s, g.lane, x, s.cur, s.prop);
   }
 
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
+  struct SCtx {  // per-update sums of the candidate-independent MvNormal terms (ir_jit.cpp mmb_jp_<b>)
+    double pre[2 * MMB_IR_SPRE];
+  };
+#else
   struct SCtx {};
+#endif
   struct SMemo {};
   struct Prep {};
 #if defined(MMB_IR_JIT) && defined(MMB_IR_SEP)
@@ -214,12 +220,18 @@ struct Mdl<MMB_MODEL_IR> {
   static constexpr bool AMWG_PROBE = false;  // (the near-threshold test hook is rats-only)
   __device__ __forceinline__ static bool amwg_sep(const DBlock& B) { return B.sep != nullptr; }
   __device__ __forceinline__ static bool slice_cand_ok(const DBlock& B) { return B.d <= SLICE_CAND_D; }
-  __device__ __forceinline__ static void slice_cand_prep(const SweepArgs&, const DBlock&, const St&, const Lc&,
-                                                         const Grp<G>&, double*, SCtx&) {}
+  __device__ __forceinline__ static void slice_cand_prep(const SweepArgs& A, const DBlock& B, const St& s, const Lc&,
+                                                         const Grp<G>& g, double*, SCtx& cx) {
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
+    mmb_jit_slice_prep(A, B.ir_blk, s.cur, g, cx.pre);
+#else
+    (void)A; (void)B; (void)s; (void)g; (void)cx;
+#endif
+  }
   // logpdf!(m, x, block) at the candidate xv (this lane's 8-lane group's), as logf: xv relisted
   // (invlinked when transformed, put()) into the coordinates' state values
   __device__ __forceinline__ static double slice_cand_logf(const SweepArgs& A, const DBlock& B, const St& s,
-                                                           const SCtx&, const double* xv, int lane, SMemo&) {
+                                                           const SCtx& cx, const double* xv, int lane, SMemo&) {
 #if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
     double c[SLICE_CAND_D];
 #pragma unroll
@@ -232,9 +244,9 @@ struct Mdl<MMB_MODEL_IR> {
         c[a] = B.transform ? mmb_ir_invlink(lk, xv[a], lo, hi) : xv[a];
       }
     }
-    return mmb_jit_slice_cand(A, B.ir_blk, s.cur, c, lane & 7, B.transform);
+    return mmb_jit_slice_cand(A, B.ir_blk, s.cur, c, lane & 7, B.transform, cx.pre);
 #else
-    (void)A; (void)B; (void)s; (void)xv; (void)lane;
+    (void)A; (void)B; (void)s; (void)cx; (void)xv; (void)lane;
     return 0.0;
 #endif
   }

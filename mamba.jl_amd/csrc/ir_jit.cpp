@@ -175,6 +175,76 @@ void gen_termw(const mmb_ir_model& ir, int n, std::ostringstream& o) {
   o << "  *c = 0.5 * fabs(" << N.len << " * MMB_LOG2PI + " << N.len << " * mmb_log(value));\n}\n";
 }
 
+// Whether expression pc reads any of `slots` (a Slice block's coordinates): a VAL of one, or an
+// indexed / gathered read of a node whose slot range holds one (an unknown base: yes)
+bool expr_reads(const mmb_ir_model& ir, int pc, const std::vector<int>& slots) {
+  auto in_node = [&](int base) {
+    for (int n = 0; n < ir.nnodes; ++n) {
+      const mmb_ir_node& N = ir.nodes[n];
+      if (N.fixed || N.off != base) continue;
+      for (int k : slots)
+        if (k >= base && k < base + N.len) return true;
+      return false;
+    }
+    return true;
+  };
+  for (;; ++pc) {
+    const uint32_t w = (uint32_t)ir.code[pc];
+    const int op = (int)(w >> 24), arg = (int)(w & 0xffffffu);
+    if (op == MMB_IR_OP_END) return false;
+    if (op == MMB_IR_OP_VAL && std::find(slots.begin(), slots.end(), arg) != slots.end()) return true;
+    if ((op == MMB_IR_OP_VALI || op == MMB_IR_OP_VALG) && in_node(arg)) return true;
+    if (op == MMB_IR_OP_VALG) ++pc;
+  }
+}
+
+// The MvNormal terms of Slice block b whose elements read none of the block's coordinates (only
+// their sigma does, e.g. rats' y term in the s2_c block): their sum of squares is the same for
+// every candidate, so mmb_jp_<b> forms it once per update with logf's own loop and 32-lane sum
+// (gen_node), and mmb_jc_<b> only evaluates d_iso at the candidate's sigma -- the same value as
+// the candidate-side loop, whose tree is logf's.
+std::vector<int> slice_shared_terms(const mmb_model_spec& spec, const mmb_ir_model& ir, int b,
+                                    const std::vector<int>& slots) {
+  const mmb_block_spec& s = spec.blocks[b];
+  const mmb_ir_block& IB = ir.blocks[b];
+  std::vector<int> out;
+  for (int t = 0; t < IB.nterms; ++t) {
+    const int n = IB.term[t];
+    const mmb_ir_node& N = ir.nodes[n];
+    if (N.family != MMB_IR_ISONORMAL) continue;
+    bool inblk = false;
+    for (int a = 0; a < s.nnodes; ++a) inblk = inblk || s.nodes[a] == n;
+    if (inblk || expr_reads(ir, N.expr[0], slots)) continue;
+    out.push_back(t);
+  }
+  return out;
+}
+
+void gen_slice_prep(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, const std::vector<int>& shared,
+                    std::ostringstream& o) {
+  (void)spec;
+  const mmb_ir_block& IB = ir.blocks[b];
+  o << "__device__ __forceinline__ void mmb_jp_" << b
+    << "(const SweepArgs& A, const double* vals, const Grp<32>& g, double* pre) {\n";
+  o << "  const int lane = g.lane;\n  (void)lane;\n";
+  int tmp = 0;
+  for (size_t j = 0; j < shared.size(); ++j) {
+    const int n = IB.term[shared[j]];
+    const mmb_ir_node& N = ir.nodes[n];
+    const std::string src = N.fixed ? "(A.ir_pool + " + std::to_string(N.off) + ")" : "(vals + " + std::to_string(N.off) + ")";
+    o << "  {  // term " << shared[j] << ": node " << n << "\n";
+    o << "    double ss = 0.0, bad = 0.0;\n";
+    o << "    for (int i = lane; i < " << N.len << "; i += 32) {\n";
+    o << "      const double x = " << src << "[i];\n";
+    const std::string m = gen_expr(ir, N.expr[0], "i", o, tmp);
+    o << "      const double r = x - " << m << ";\n";
+    o << "      ss = ss + r * r;\n      bad = isfinite(x) ? bad : 1.0;\n    }\n";
+    o << "    g.sum2(ss, bad);\n";
+    o << "    pre[" << 2 * j << "] = ss;\n    pre[" << 2 * j + 1 << "] = bad;\n  }\n";
+  }
+  o << "}\n";
+}
+
 // logpdf!(m, x, block) of Slice block b at one candidate per 8-lane group (samplers.h
 // slice_uni_cand / slice_multi_cand; ir.h slice_cand_logf): the block's coordinates are read from
 // c[] (state values, invlinked) instead of the chain state.  Lane r of the group stands for lanes
@@ -182,17 +252,24 @@ void gen_termw(const mmb_ir_model& ir, int n, std::ostringstream& o) {
 // .. in order, as gen_node's loop) and combines them as levels 0-1 of the 32-lane butterfly, ((p0 +
 // p1) + (p2 + p3)); levels 2-4 are xor 1, 2, 4 across the group (DPP, as Grp<32>::sum's half-mirror
 // and mirror stages after quads agree).  The same tree over the same terms: bit-identical to logf.
-void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, std::ostringstream& o) {
+std::vector<int> block_slots(const mmb_model_spec& spec, const mmb_ir_model& ir, int b) {
   const mmb_block_spec& s = spec.blocks[b];
-  const mmb_ir_block& IB = ir.blocks[b];
   std::vector<int> slots;
   for (int a = 0; a < s.nnodes; ++a) {
     const mmb_ir_node& N = ir.nodes[s.nodes[a]];
     for (int q = 0; q < N.len; ++q) slots.push_back(N.off + q);
   }
+  return slots;
+}
+
+void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, const std::vector<int>& shared,
+                    std::ostringstream& o) {
+  const mmb_block_spec& s = spec.blocks[b];
+  const mmb_ir_block& IB = ir.blocks[b];
+  const std::vector<int> slots = block_slots(spec, ir, b);
   o << "__device__ __forceinline__ double mmb_jc_" << b << "(const SweepArgs& A, const double* vals, const double* c, int r,\n"
-       "                                        int transform) {\n";
-  o << "  (void)transform;\n";
+       "                                        int transform, const double* pre) {\n";
+  o << "  (void)transform; (void)pre;\n";
   o << "  auto rd = [&](int k) -> double {\n    return ";
   for (size_t a = 0; a < slots.size(); ++a) o << "k == " << slots[a] << " ? c[" << a << "] : ";
   o << "vals[k];\n  };\n  (void)rd;\n";
@@ -210,7 +287,14 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, s
       return "vals[" + std::to_string(N.off) + " + " + i + "]";
     };
     o << "  {  // term " << t << ": node " << n << "\n";
-    if (N.family == MMB_IR_ISONORMAL) {
+    const auto sh = std::find(shared.begin(), shared.end(), t);
+    if (sh != shared.end()) {  // elements independent of the candidate: mmb_jp_<b>'s sums
+      const int j = (int)(sh - shared.begin());
+      o << "    double sig;\n    {\n    const int i = 0;\n    (void)i;\n";
+      const std::string sg = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
+      o << "    sig = " << sg << ";\n    }\n";
+      o << "    lp += pre[" << 2 * j + 1 << "] != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, pre[" << 2 * j << "]);\n";
+    } else if (N.family == MMB_IR_ISONORMAL) {
       o << "    double sig;\n    {\n    const int i = 0;\n    (void)i;\n";
       const std::string sg = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
       o << "    sig = " << sg << ";\n    }\n";
@@ -345,25 +429,41 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
   }
   {  // Slice blocks of up to four coordinates: candidates evaluated four at a time (ir.h)
     bool any = false;
+    int npre = 0;
     for (int b = 0; b < spec.nblocks; ++b) {
       if (spec.blocks[b].sampler != MMB_SAMPLER_SLICE) continue;
       int d = 0;
       for (int a = 0; a < spec.blocks[b].nnodes; ++a) d += ir.nodes[spec.blocks[b].nodes[a]].len;
       if (d > 4) continue;
-      gen_slice_cand(spec, ir, b, o);
+      const std::vector<int> shared = slice_shared_terms(spec, ir, b, block_slots(spec, ir, b));
+      if (!shared.empty()) gen_slice_prep(spec, ir, b, shared, o);
+      npre = std::max(npre, (int)shared.size());
+      gen_slice_cand(spec, ir, b, shared, o);
       any = true;
     }
     if (any) {
-      o << "#define MMB_IR_SLICEC 1\n";
+      o << "#define MMB_IR_SLICEC 1\n#define MMB_IR_SPRE " << std::max(npre, 1) << "\n";
+      o << "__device__ __forceinline__ void mmb_jit_slice_prep(const SweepArgs& A, int blk, const double* vals,\n"
+           "                                                   const Grp<32>& g, double* pre) {\n"
+           "  (void)A; (void)vals; (void)g; (void)pre;\n  switch (blk) {\n";
+      for (int b = 0; b < spec.nblocks; ++b) {
+        if (spec.blocks[b].sampler != MMB_SAMPLER_SLICE) continue;
+        int d = 0;
+        for (int a = 0; a < spec.blocks[b].nnodes; ++a) d += ir.nodes[spec.blocks[b].nodes[a]].len;
+        if (d > 4 || slice_shared_terms(spec, ir, b, block_slots(spec, ir, b)).empty()) continue;
+        o << "    case " << b << ": mmb_jp_" << b << "(A, vals, g, pre); return;\n";
+      }
+      o << "    default: return;\n  }\n}\n";
       o << "__device__ __forceinline__ double mmb_jit_slice_cand(const SweepArgs& A, int blk, const double* vals,\n"
-           "                                                     const double* c, int r, int transform) {\n"
+           "                                                     const double* c, int r, int transform,\n"
+           "                                                     const double* pre) {\n"
            "  switch (blk) {\n";
       for (int b = 0; b < spec.nblocks; ++b) {
         if (spec.blocks[b].sampler != MMB_SAMPLER_SLICE) continue;
         int d = 0;
         for (int a = 0; a < spec.blocks[b].nnodes; ++a) d += ir.nodes[spec.blocks[b].nodes[a]].len;
         if (d > 4) continue;
-        o << "    case " << b << ": return mmb_jc_" << b << "(A, vals, c, r, transform);\n";
+        o << "    case " << b << ": return mmb_jc_" << b << "(A, vals, c, r, transform, pre);\n";
       }
       o << "    default: return __builtin_nan(\"\");\n  }\n}\n";
     }
@@ -410,6 +510,10 @@ int mmb_ir_jit_obtain(const std::string& src, std::vector<char>* code, std::stri
   h = fnv1a(h, &mnr, sizeof mnr);
   char name[64];
   snprintf(name, sizeof name, "irjit_%016llx.co", (unsigned long long)h);
+  if (const char* dump = std::getenv("MMB_JIT_DUMP")) {  // (inspection: the generated source)
+    std::ofstream f(dump);
+    if (f) f << src;
+  }
   const char* env = std::getenv("MMB_JIT_CACHE");
   const std::string dir = env && *env ? std::string(env) : lib_dir() + "/jit";
   const std::string path = dir + "/" + name;
