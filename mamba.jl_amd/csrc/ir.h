@@ -201,6 +201,9 @@ struct Mdl<MMB_MODEL_IR> {
     put(B, s, g.lane, x, s.cur, s.prop);
   }
 
+#ifndef MMB_IR_LOGF_ATTR
+#define MMB_IR_LOGF_ATTR  // logf is called, not inlined (ir_jit.cpp: MMB_IR_LOGF_INLINE)
+#endif
 #if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
   struct SCtx {  // per-update sums of the candidate-independent MvNormal terms (ir_jit.cpp mmb_jp_<b>)
     double pre[2 * MMB_IR_SPRE];
@@ -326,7 +329,7 @@ struct Mdl<MMB_MODEL_IR> {
   static constexpr int SLICE_NC = 4;
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   // logpdf!(m, x, block, transform)
-  __device__ static double logf(const SweepArgs& A, const DBlock& B, const St& s, const Lc&, const Grp<G>& g,
+  __device__ MMB_IR_LOGF_ATTR static double logf(const SweepArgs& A, const DBlock& B, const St& s, const Lc&, const Grp<G>& g,
                                 const double* x) {
     put(B, s, g.lane, x, s.prop, nullptr);
 #ifdef MMB_IR_JIT

@@ -363,8 +363,14 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
   // straight-line model code fits 128 VGPRs where the interpreter needed 2 waves' budget)
   int waves = 4;
   if (const char* w = std::getenv("MMB_IR_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(w)));
-  o << "#define MMB_IR_JIT 1\n#define MMB_IR_DMAX " << dmax << "\n#define MMB_IR_WAVES " << waves
-    << "\n#include \"device.h\"\n\n";
+  o << "#define MMB_IR_JIT 1\n#define MMB_IR_DMAX " << dmax << "\n#define MMB_IR_WAVES " << waves << "\n";
+  {  // logf inlined at its call sites: a call makes the caller save and restore its SGPRs around
+     // it (rats via the IR: 689 -> 509 SGPR spill slots, 6.1e7 -> 7.4e7 chain-updates/s A/B);
+     // MMB_IR_LOGF_INLINE=0 keeps the call
+    const char* e = std::getenv("MMB_IR_LOGF_INLINE");
+    if (!(e && std::atoi(e) == 0)) o << "#define MMB_IR_LOGF_ATTR __forceinline__\n";
+  }
+  o << "#include \"device.h\"\n\n";
   // a uniform pool value (scalar load): data may change between models of the same structure,
   // so the source -- and the cached code object -- depends on the model's structure only
   o << "__device__ __forceinline__ double mmb_jit_uload(const double* p, int k) {\n"
