@@ -247,7 +247,7 @@ struct Mdl<MMB_MODEL_IR> {
         c[a] = B.transform ? mmb_ir_invlink(lk, xv[a], lo, hi) : xv[a];
       }
     }
-    return mmb_jit_slice_cand(A, B.ir_blk, s.cur, c, lane & 7, B.transform, cx.pre);
+    return mmb_jit_slice_cand(A, B.ir_blk, s.cur, c, lane & (32 / SLICE_NC - 1), B.transform, cx.pre);
 #else
     (void)A; (void)B; (void)s; (void)cx; (void)xv; (void)lane;
     return 0.0;
@@ -326,7 +326,10 @@ struct Mdl<MMB_MODEL_IR> {
   static constexpr bool SLICE_CAND = false;  // samplers.h slice_uni: one candidate at a time
 #endif
   static constexpr int SLICE_CAND_D = 2;
-  static constexpr int SLICE_NC = 4;
+#ifndef MMB_IR_SLICE_NC
+#define MMB_IR_SLICE_NC 4
+#endif
+  static constexpr int SLICE_NC = MMB_IR_SLICE_NC;  // candidates per round (ir_jit.cpp: 2 or 4)
   __device__ __forceinline__ static Prep prep(const DBlock&, const St&) { return Prep{}; }
   // logpdf!(m, x, block, transform)
   __device__ MMB_IR_LOGF_ATTR static double logf(const SweepArgs& A, const DBlock& B, const St& s, const Lc&, const Grp<G>& g,

@@ -245,13 +245,15 @@ void gen_slice_prep(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, c
   o << "}\n";
 }
 
-// logpdf!(m, x, block) of Slice block b at one candidate per 8-lane group (samplers.h
+// logpdf!(m, x, block) of Slice block b at one candidate per group of 32 / VL lanes (samplers.h
 // slice_uni_cand / slice_multi_cand; ir.h slice_cand_logf): the block's coordinates are read from
 // c[] (state values, invlinked) instead of the chain state.  Lane r of the group stands for lanes
-// 4r .. 4r+3 of the 32-lane layout: it forms their four lane partials (elements i = lane, lane + 32,
-// .. in order, as gen_node's loop) and combines them as levels 0-1 of the 32-lane butterfly, ((p0 +
-// p1) + (p2 + p3)); levels 2-4 are xor 1, 2, 4 across the group (DPP, as Grp<32>::sum's half-mirror
-// and mirror stages after quads agree).  The same tree over the same terms: bit-identical to logf.
+// VL r .. VL r + VL - 1 of the 32-lane layout: it forms their VL lane partials (elements i = lane,
+// lane + 32, .. in order, as gen_node's loop) and combines them as the first log2(VL) levels of the
+// 32-lane butterfly -- (p0 + p1), or ((p0 + p1) + (p2 + p3)) for VL = 4; the remaining levels are
+// Grp<32>::other_d<0..> across the group (after the local levels every lane's virtual lanes agree,
+// so each later partner lane of Grp<32>::sum's tree is reached by the next stage's partner of the
+// real lane).  The same tree over the same terms: bit-identical to logf.
 std::vector<int> block_slots(const mmb_model_spec& spec, const mmb_ir_model& ir, int b) {
   const mmb_block_spec& s = spec.blocks[b];
   std::vector<int> slots;
@@ -263,7 +265,7 @@ std::vector<int> block_slots(const mmb_model_spec& spec, const mmb_ir_model& ir,
 }
 
 void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, const std::vector<int>& shared,
-                    std::ostringstream& o) {
+                    int VL, std::ostringstream& o) {
   const mmb_block_spec& s = spec.blocks[b];
   const mmb_ir_block& IB = ir.blocks[b];
   const std::vector<int> slots = block_slots(spec, ir, b);
@@ -299,22 +301,21 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, c
       const std::string sg = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
       o << "    sig = " << sg << ";\n    }\n";
       o << "    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0, bd = 0.0;\n";
-      o << "#pragma nounroll\n    for (int v = 0; v < 4; ++v) {\n      double ss = 0.0;\n";
-      o << "      for (int i = 4 * r + v; i < " << N.len << "; i += 32) {\n";
+      o << "#pragma nounroll\n    for (int v = 0; v < " << VL << "; ++v) {\n      double ss = 0.0;\n";
+      o << "      for (int i = " << VL << " * r + v; i < " << N.len << "; i += 32) {\n";
       o << "        const double x = " << xval("i") << ";\n";
       const std::string m = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
       o << "        const double rr = x - " << m << ";\n        ss = ss + rr * rr;\n";
       o << "        bd = isfinite(x) ? bd : 1.0;\n      }\n";
       o << "      p0 = v == 0 ? ss : p0;\n      p1 = v == 1 ? ss : p1;\n      p2 = v == 2 ? ss : p2;\n      p3 = v == 3 ? ss : p3;\n    }\n";
-      o << "    double sv = (p0 + p1) + (p2 + p3);\n";
-      o << "    sv += Grp<32>::other_d<0>(sv); bd += Grp<32>::other_d<0>(bd);\n";
-      o << "    sv += Grp<32>::other_d<1>(sv); bd += Grp<32>::other_d<1>(bd);\n";
-      o << "    sv += Grp<32>::other_d<2>(sv); bd += Grp<32>::other_d<2>(bd);\n";
+      o << (VL == 4 ? "    double sv = (p0 + p1) + (p2 + p3);\n" : "    double sv = p0 + p1;\n");
+      for (int k = 0; k < 5 - (VL == 4 ? 2 : 1); ++k)
+        o << "    sv += Grp<32>::other_d<" << k << ">(sv); bd += Grp<32>::other_d<" << k << ">(bd);\n";
       o << "    lp += bd != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, sv);\n";
     } else {
       o << "    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;\n";
-      o << "#pragma nounroll\n    for (int v = 0; v < 4; ++v) {\n      double acc = 0.0;\n";
-      o << "      for (int i = 4 * r + v; i < " << N.len << "; i += 32) {\n";
+      o << "#pragma nounroll\n    for (int v = 0; v < " << VL << "; ++v) {\n      double acc = 0.0;\n";
+      o << "      for (int i = " << VL << " * r + v; i < " << N.len << "; i += 32) {\n";
       std::string a = "0.0", bb = "0.0", ct = "0.0";
       if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
       if (N.expr[1] >= 0) bb = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
@@ -322,8 +323,8 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, c
       o << "        acc = acc + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
         << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n      }\n";
       o << "      p0 = v == 0 ? acc : p0;\n      p1 = v == 1 ? acc : p1;\n      p2 = v == 2 ? acc : p2;\n      p3 = v == 3 ? acc : p3;\n    }\n";
-      o << "    double sv = (p0 + p1) + (p2 + p3);\n";
-      o << "    sv += Grp<32>::other_d<0>(sv);\n    sv += Grp<32>::other_d<1>(sv);\n    sv += Grp<32>::other_d<2>(sv);\n";
+      o << (VL == 4 ? "    double sv = (p0 + p1) + (p2 + p3);\n" : "    double sv = p0 + p1;\n");
+      for (int k = 0; k < 5 - (VL == 4 ? 2 : 1); ++k) o << "    sv += Grp<32>::other_d<" << k << ">(sv);\n";
       o << "    lp += sv;\n";
     }
     o << "    if (!isfinite(lp)) return lp;\n  }\n";
@@ -436,6 +437,11 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
   {  // Slice blocks of up to four coordinates: candidates evaluated four at a time (ir.h)
     bool any = false;
     int npre = 0;
+    // candidates per round = virtual lanes per lane: 2 (sixteen lanes per candidate; default) or 4
+    // (eight; MMB_IR_SLICE_NC=4).  rats via the IR: 7.52e7 (2) vs 7.15e7 (4) chain-updates/s A/B --
+    // the scalar blocks accept within a candidate or two, so wider rounds mostly add work
+    int nc = 2;
+    if (const char* e = std::getenv("MMB_IR_SLICE_NC")) nc = std::atoi(e) == 4 ? 4 : 2;
     for (int b = 0; b < spec.nblocks; ++b) {
       if (spec.blocks[b].sampler != MMB_SAMPLER_SLICE) continue;
       int d = 0;
@@ -444,11 +450,11 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
       const std::vector<int> shared = slice_shared_terms(spec, ir, b, block_slots(spec, ir, b));
       if (!shared.empty()) gen_slice_prep(spec, ir, b, shared, o);
       npre = std::max(npre, (int)shared.size());
-      gen_slice_cand(spec, ir, b, shared, o);
+      gen_slice_cand(spec, ir, b, shared, nc, o);
       any = true;
     }
     if (any) {
-      o << "#define MMB_IR_SLICEC 1\n#define MMB_IR_SPRE " << std::max(npre, 1) << "\n";
+      o << "#define MMB_IR_SLICEC 1\n#define MMB_IR_SPRE " << std::max(npre, 1) << "\n#define MMB_IR_SLICE_NC " << nc << "\n";
       o << "__device__ __forceinline__ void mmb_jit_slice_prep(const SweepArgs& A, int blk, const double* vals,\n"
            "                                                   const Grp<32>& g, double* pre) {\n"
            "  (void)A; (void)vals; (void)g; (void)pre;\n  switch (blk) {\n";

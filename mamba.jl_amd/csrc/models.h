@@ -312,7 +312,7 @@ struct Mdl<MMB_MODEL_RATS> {
 #endif
   // candidates per round: NC groups of 32 / NC lanes, NC leaves (rats) per lane
   static constexpr int SLICE_NC = MMB_SLICE_NC;
-  static_assert(SLICE_NC == 4 || SLICE_NC == 8, "4 or 8 candidates per round");
+  static_assert(SLICE_NC == 2 || SLICE_NC == 4 || SLICE_NC == 8, "2, 4 or 8 candidates per round");
   struct SCtx {
     const double* ab;  // LDS: alpha[32] | beta[32] of the chain
     double ss;         // y's residual sum of squares (alpha, beta are not in the block)
@@ -336,7 +336,8 @@ struct Mdl<MMB_MODEL_RATS> {
     grp_sync();
   }
   // normsum_lane + g.sum over the candidate group (see above); v: alpha or beta in LDS.  NC = 8:
-  // groups of four lanes with eight leaves each, levels 0-2 in the lane, 3-4 by xor 1 and xor 2.
+  // groups of four lanes with eight leaves each, levels 0-2 in the lane, 3-4 by xor 1 and xor 2;
+  // NC = 2: groups of sixteen lanes with two leaves each, level 0 in the lane, 1-4 across it.
   __device__ __forceinline__ static double normsum_grp8(double mu, double sig, double logsig, const double* v,
                                                         int lane) {
     constexpr int L = SLICE_NC, LPC = 32 / SLICE_NC;
@@ -348,11 +349,17 @@ struct Mdl<MMB_MODEL_RATS> {
       lf[m] = 0.0 + (r0 + m < 30 ? d_normlogpdf(mu, sig, logsig, p.x) : 0.0);
       lf[m + 1] = 0.0 + (r0 + m + 1 < 30 ? d_normlogpdf(mu, sig, logsig, p.y) : 0.0);
     }
-    double q = (lf[0] + lf[1]) + (lf[2] + lf[3]);
-    if constexpr (L == 8) q = q + ((lf[4] + lf[5]) + (lf[6] + lf[7]));
+    double q;
+    if constexpr (L == 2) {
+      q = lf[0] + lf[1];
+    } else {
+      q = (lf[0] + lf[1]) + (lf[2] + lf[3]);
+      if constexpr (L == 8) q = q + ((lf[4] + lf[5]) + (lf[6] + lf[7]));
+    }
     q += Grp<G>::template other_d<0>(q);
     q += Grp<G>::template other_d<1>(q);
-    if constexpr (LPC == 8) q += Grp<G>::template other_d<2>(q);
+    if constexpr (LPC >= 8) q += Grp<G>::template other_d<2>(q);
+    if constexpr (LPC >= 16) q += Grp<G>::template other_d<3>(q);
     return q;
   }
   // The pieces of slice_cand_logf that only depend on one node value -- each block node's prior

@@ -1419,7 +1419,7 @@ struct Smp {
                                                         St& s, const Lc& l, const Grp<G>& g, double* lds) {
     constexpr int SD = M::SLICE_CAND_D;
     constexpr int NC = M::SLICE_NC, LPC = 32 / NC;  // candidates per round, lanes per candidate
-    constexpr uint32_t LEAD = NC == 4 ? 0x01010101u : 0x11111111u;  // group leaders' ballot bits
+    constexpr uint32_t LEAD = NC == 2 ? 0x00010001u : NC == 4 ? 0x01010101u : 0x11111111u;  // group leaders' ballot bits
     static_assert(MMB_SLICE_MAX_SHRINK % NC == 0, "rounds of candidates end at the cap");
     const int d = B.d;
     double x[R];
@@ -1578,7 +1578,7 @@ struct Smp {
       }
     }
     constexpr int NC = M::SLICE_NC, LPC = 32 / NC;
-    constexpr uint32_t LEAD = NC == 4 ? 0x01010101u : 0x11111111u;
+    constexpr uint32_t LEAD = NC == 2 ? 0x00010001u : NC == 4 ? 0x01010101u : 0x11111111u;
     const int q = g.lane / LPC;
     const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
     double prev[SD], xn[SD];
