@@ -120,6 +120,19 @@ void gen_node(const mmb_ir_model& ir, int n, std::ostringstream& o) {
     o << "  return bad != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, ss);\n}\n";
     return;
   }
+  if (N.len == 1) {
+    // one element: every lane forms it (no lane partials, no butterfly).  The butterfly over lane
+    // 0's term and 31 zeros returns the term itself except that -0 becomes +0, and the block's
+    // running lp -- which starts at +0 and so is never -0 -- adds either to the same value
+    o << "  (void)lane;\n  const int i = 0;\n";
+    std::string a = "0.0", b = "0.0", ct = "0.0";
+    if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp);
+    if (N.expr[1] >= 0) b = gen_expr(ir, N.expr[1], "i", o, tmp);
+    if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
+    o << "  return 0.0 + mmb_ir_lp(" << N.family << ", " << src << "[i], " << a << ", " << b << ", " << ct
+      << ", tr, " << lit(N.lo) << ", " << lit(N.hi) << ");\n}\n";
+    return;
+  }
   o << "  double acc = 0.0;\n";
   o << "  for (int i = lane; i < " << N.len << "; i += 32) {\n";
   std::string a = "0.0", b = "0.0", ct = "0.0";
@@ -312,6 +325,14 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, c
       for (int k = 0; k < 5 - (VL == 4 ? 2 : 1); ++k)
         o << "    sv += Grp<32>::other_d<" << k << ">(sv); bd += Grp<32>::other_d<" << k << ">(bd);\n";
       o << "    lp += bd != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, sv);\n";
+    } else if (N.len == 1) {  // one element: on every lane, as gen_node
+      o << "    {\n    const int i = 0;\n";
+      std::string a = "0.0", bb = "0.0", ct = "0.0";
+      if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
+      if (N.expr[1] >= 0) bb = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
+      if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
+      o << "    lp += 0.0 + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
+        << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n    }\n";
     } else {
       o << "    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;\n";
       o << "#pragma nounroll\n    for (int v = 0; v < " << VL << "; ++v) {\n      double acc = 0.0;\n";
