@@ -231,6 +231,20 @@ struct Mdl<MMB_MODEL_IR> {
     (void)A; (void)B; (void)s; (void)g; (void)cx;
 #endif
   }
+  // logf at the start of a Slice update, after slice_cand_prep: blocks with candidate-independent
+  // MvNormal terms take their sums of squares from the prep (ir_jit.cpp mmb_jit_block_lp_pre)
+  __device__ __forceinline__ static double slice_logf0(const SweepArgs& A, const DBlock& B, const St& s, const Lc& l,
+                                                       const Grp<G>& g, const double* x, const SCtx& cx) {
+#if defined(MMB_IR_JIT) && defined(MMB_IR_SLICEC)
+    if (mmb_jit_slice_has_pre(B.ir_blk)) {
+      put(B, s, g.lane, x, s.prop, nullptr);
+      return mmb_jit_block_lp_pre(A, B.ir_blk, s.prop, g, B.transform, cx.pre);
+    }
+#else
+    (void)cx;
+#endif
+    return logf(A, B, s, l, g, x);
+  }
   // logpdf!(m, x, block) at the candidate xv (this lane's 8-lane group's), as logf: xv relisted
   // (invlinked when transformed, put()) into the coordinates' state values
   __device__ __forceinline__ static double slice_cand_logf(const SweepArgs& A, const DBlock& B, const St& s,

@@ -458,6 +458,7 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
   {  // Slice blocks of up to four coordinates: candidates evaluated four at a time (ir.h)
     bool any = false;
     int npre = 0;
+    std::vector<int> pre_blocks;  // Slice candidate blocks with shared MvNormal sums
     // candidates per round = virtual lanes per lane: 2 (sixteen lanes per candidate; default) or 4
     // (eight; MMB_IR_SLICE_NC=4).  rats via the IR: 7.52e7 (2) vs 7.15e7 (4) chain-updates/s A/B --
     // the scalar blocks accept within a candidate or two, so wider rounds mostly add work
@@ -469,7 +470,10 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
       for (int a = 0; a < spec.blocks[b].nnodes; ++a) d += ir.nodes[spec.blocks[b].nodes[a]].len;
       if (d > 4) continue;
       const std::vector<int> shared = slice_shared_terms(spec, ir, b, block_slots(spec, ir, b));
-      if (!shared.empty()) gen_slice_prep(spec, ir, b, shared, o);
+      if (!shared.empty()) {
+        gen_slice_prep(spec, ir, b, shared, o);
+        pre_blocks.push_back(b);
+      }
       npre = std::max(npre, (int)shared.size());
       gen_slice_cand(spec, ir, b, shared, nc, o);
       any = true;
@@ -487,6 +491,36 @@ std::string mmb_ir_jit_source(const mmb_model_spec& spec, const mmb_ir_model& ir
         o << "    case " << b << ": mmb_jp_" << b << "(A, vals, g, pre); return;\n";
       }
       o << "    default: return;\n  }\n}\n";
+      o << "__device__ __forceinline__ bool mmb_jit_slice_has_pre(int blk) {\n  switch (blk) {\n";
+      for (int b : pre_blocks) o << "    case " << b << ": return true;\n";
+      o << "    default: return false;\n  }\n}\n";
+      // logpdf!(m, x, block) as mmb_jit_block_lp, the shared MvNormal terms from the prep's sums
+      o << "__device__ __forceinline__ double mmb_jit_block_lp_pre(const SweepArgs& A, int blk, const double* vals,\n"
+           "                                                       const Grp<32>& g, int transform, const double* pre) {\n"
+           "  (void)transform;\n  double lp = 0.0;\n  switch (blk) {\n";
+      for (int b : pre_blocks) {
+        const mmb_ir_block& IB = ir.blocks[b];
+        const std::vector<int> shared = slice_shared_terms(spec, ir, b, block_slots(spec, ir, b));
+        o << "    case " << b << ":\n";
+        for (int t = 0; t < IB.nterms; ++t) {
+          const auto sh = std::find(shared.begin(), shared.end(), t);
+          if (sh == shared.end()) {
+            o << "      lp += mmb_jn_" << IB.term[t] << "(A, vals, g, " << (IB.trans[t] ? "transform" : "0") << ");\n";
+          } else {  // gen_node's MvNormal with the prep's (ss, bad)
+            const int j = (int)(sh - shared.begin());
+            const mmb_ir_node& N = ir.nodes[IB.term[t]];
+            int tmp = 0;
+            o << "      {\n      double sig;\n      {\n      const int i = 0;\n      (void)i;\n";
+            const std::string sg = gen_expr(ir, N.expr[1], "i", o, tmp);
+            o << "      sig = " << sg << ";\n      }\n";
+            o << "      lp += pre[" << 2 * j + 1 << "] != 0.0 ? -__builtin_inf() : d_iso(" << N.len << ", sig, pre["
+              << 2 * j << "]);\n      }\n";
+          }
+          o << "      if (!isfinite(lp)) break;\n";
+        }
+        o << "      break;\n";
+      }
+      o << "    default: break;\n  }\n  return lp;\n}\n";
       o << "__device__ __forceinline__ double mmb_jit_slice_cand(const SweepArgs& A, int blk, const double* vals,\n"
            "                                                     const double* c, int r, int transform,\n"
            "                                                     const double* pre) {\n"

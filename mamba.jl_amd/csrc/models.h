@@ -260,8 +260,9 @@ struct Mdl<MMB_MODEL_RATS> {
     lv = logf_p(A, B, c, s, l, g, v);
   }
   // logpdf!(block, x)
+  // (ssp: y's residual sum of squares already formed from this state -- slice_logf0)
   __device__ __forceinline__ static double logf(const SweepArgs& A, const DBlock& B, const St& s0, const Lc& l,
-                                const Grp<G>& g, const double* x) {
+                                const Grp<G>& g, const double* x, const double* ssp = nullptr) {
     St s = s0;
     relist(B, s, g, x);
     if (is_vec(B.nodes[0])) return logf_vec(A, vec_ctx(B, s0), s0, l, g, x);
@@ -293,7 +294,7 @@ struct Mdl<MMB_MODEL_RATS> {
       if (!isfinite(lp)) return lp;
     }
     if (tm & 4u) {
-      double ss = g.sum(ssr_lane(A, l, s.a, s.b, g.lane));
+      double ss = ssp ? *ssp : g.sum(ssr_lane(A, l, s.a, s.b, g.lane));
       lp += d_iso(150, sqrt(s.s2c), ss);
     }
     return lp;
@@ -392,6 +393,12 @@ struct Mdl<MMB_MODEL_RATS> {
       }
     }
   };
+  // logf at the start of a Slice update, after slice_cand_prep: the s2_c block takes y's sum of
+  // squares from the prep (the same g.sum over the same lane terms: alpha and beta are not in the block)
+  __device__ __forceinline__ static double slice_logf0(const SweepArgs& A, const DBlock& B, const St& s, const Lc& l,
+                                                       const Grp<G>& g, const double* x, const SCtx& c) {
+    return logf(A, B, s, l, g, x, (c.tm & 4u) ? &c.ss : nullptr);
+  }
   // logf(block) at the block vector xv[] (group-uniform values, the candidate's)
   __device__ __forceinline__ static double slice_cand_logf(const SweepArgs& A, const DBlock& B, const St& s0,
                                                            const SCtx& c, const double* xv, int lane, SMemo& mm) {

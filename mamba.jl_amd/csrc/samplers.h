@@ -1424,15 +1424,19 @@ struct Smp {
     const int d = B.d;
     double x[R];
     M::unlist(B, s, g.lane, x);
+    typename M::SCtx cx;
+    M::slice_cand_prep(A, B, s, l, g, lds, cx);
+#ifndef MMB_EXP_SLICE_LOGF  // (experiment: logf recomputing every sum)
+    double logf0 = M::slice_logf0(A, B, s, l, g, x, cx);  // logf, reusing the prep's sums
+#else
     double logf0 = M::logf(A, B, s, l, g, x);
+#endif
     double lo = 0.0, up = 0.0;
     if (g.lane < d) {
       const double w = width(B, g.lane);
       lo = x[0] - w * mmb_uniform(&ru, (uint32_t)g.lane);
       up = lo + w;
     }
-    typename M::SCtx cx;
-    M::slice_cand_prep(A, B, s, l, g, lds, cx);
     typename M::SMemo memo;
     double xu[SD], lou[SD], upu[SD];  // element values and intervals, group-uniform
 #pragma unroll
@@ -1561,9 +1565,13 @@ struct Smp {
     double v[R];
     M::unlist(B, s, g.lane, v);
     UWin uw{0.0, 0xffffffffu - (uint32_t)G};
-    const double p0 = M::logf(A, B, s, l, g, v) + mmb_log(uwin_next(ru, uw, 0u, g));
     typename M::SCtx cx;
     M::slice_cand_prep(A, B, s, l, g, lds, cx);
+#ifndef MMB_EXP_SLICE_LOGF
+    const double p0 = M::slice_logf0(A, B, s, l, g, v, cx) + mmb_log(uwin_next(ru, uw, 0u, g));
+#else
+    const double p0 = M::logf(A, B, s, l, g, v) + mmb_log(uwin_next(ru, uw, 0u, g));
+#endif
     typename M::SMemo memo;
     double vu[SD], lo[SD], up[SD], x1[SD];
 #pragma unroll
