@@ -98,6 +98,17 @@ std::string gen_expr(const mmb_ir_model& ir, int pc, const std::string& idx, std
   return st.back();
 }
 
+// Whether expression pc depends on the element index (indexed / gathered state, indexed data)
+bool expr_indexed(const mmb_ir_model& ir, int pc) {
+  for (;; ++pc) {
+    const uint32_t w = (uint32_t)ir.code[pc];
+    const int op = (int)(w >> 24);
+    if (op == MMB_IR_OP_END) return false;
+    if (op == MMB_IR_OP_VALI || op == MMB_IR_OP_VALG || op == MMB_IR_OP_DATA) return true;
+    if (op == MMB_IR_OP_VALG) ++pc;
+  }
+}
+
 // logpdf(node[, transform]) of node n as the interpreter's node_lp (ir.h), group-uniform
 void gen_node(const mmb_ir_model& ir, int n, std::ostringstream& o) {
   const mmb_ir_node& N = ir.nodes[n];
@@ -131,6 +142,18 @@ void gen_node(const mmb_ir_model& ir, int n, std::ostringstream& o) {
     if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
     o << "  return 0.0 + mmb_ir_lp(" << N.family << ", " << src << "[i], " << a << ", " << b << ", " << ct
       << ", tr, " << lit(N.lo) << ", " << lit(N.hi) << ");\n}\n";
+    return;
+  }
+  if (N.family == MMB_IR_NORMAL && N.expr[1] >= 0 && !expr_indexed(ir, N.expr[1])) {
+    // sigma the same for every element: it and its log formed once (mmb_ir_normal_lb)
+    o << "  double sg, lsg;\n  {\n    const int i = 0;\n    (void)i;\n";
+    const std::string b = gen_expr(ir, N.expr[1], "i", o, tmp);
+    o << "    sg = " << b << ";\n    lsg = mmb_log(sg);\n  }\n";
+    o << "  double acc = 0.0;\n";
+    o << "  for (int i = lane; i < " << N.len << "; i += 32) {\n";
+    const std::string a = N.expr[0] >= 0 ? gen_expr(ir, N.expr[0], "i", o, tmp) : "0.0";
+    o << "    acc = acc + mmb_ir_normal_lb(" << src << "[i], " << a << ", sg, lsg);\n  }\n";
+    o << "  return g.sum(acc);\n}\n";
     return;
   }
   o << "  double acc = 0.0;\n";
@@ -334,15 +357,25 @@ void gen_slice_cand(const mmb_model_spec& spec, const mmb_ir_model& ir, int b, c
       o << "    lp += 0.0 + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
         << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n    }\n";
     } else {
+      const bool hoist = N.family == MMB_IR_NORMAL && N.expr[1] >= 0 && !expr_indexed(ir, N.expr[1]);
+      if (hoist) {  // sigma and its log once per lane (as gen_node)
+        o << "    double sg, lsg;\n    {\n    const int i = 0;\n    (void)i;\n";
+        const std::string bs = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
+        o << "    sg = " << bs << ";\n    lsg = mmb_log(sg);\n    }\n";
+      }
       o << "    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;\n";
       o << "#pragma nounroll\n    for (int v = 0; v < " << VL << "; ++v) {\n      double acc = 0.0;\n";
       o << "      for (int i = " << VL << " * r + v; i < " << N.len << "; i += 32) {\n";
       std::string a = "0.0", bb = "0.0", ct = "0.0";
       if (N.expr[0] >= 0) a = gen_expr(ir, N.expr[0], "i", o, tmp, &slots);
-      if (N.expr[1] >= 0) bb = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
-      if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
-      o << "        acc = acc + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
-        << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n      }\n";
+      if (hoist) {
+        o << "        acc = acc + mmb_ir_normal_lb(" << xval("i") << ", " << a << ", sg, lsg);\n      }\n";
+      } else {
+        if (N.expr[1] >= 0) bb = gen_expr(ir, N.expr[1], "i", o, tmp, &slots);
+        if (N.cterm >= 0) ct = "A.ir_pool[" + std::to_string(N.cterm) + " + i]";
+        o << "        acc = acc + mmb_ir_lp(" << N.family << ", " << xval("i") << ", " << a << ", " << bb << ", " << ct
+          << ", " << tr << ", " << lit(N.lo) << ", " << lit(N.hi) << ");\n      }\n";
+      }
       o << "      p0 = v == 0 ? acc : p0;\n      p1 = v == 1 ? acc : p1;\n      p2 = v == 2 ? acc : p2;\n      p3 = v == 3 ? acc : p3;\n    }\n";
       o << (VL == 4 ? "    double sv = (p0 + p1) + (p2 + p3);\n" : "    double sv = p0 + p1;\n");
       for (int k = 0; k < 5 - (VL == 4 ? 2 : 1); ++k) o << "    sv += Grp<32>::other_d<" << k << ">(sv);\n";

@@ -80,6 +80,14 @@ MMB_HD double mmb_ir_invlink(int kind, double x, double a, double b) {
  * insupport(d, x) ? logpdf(d, x[, transform]) : -Inf.  (a, b) = the family's parameters in
  * Distributions order; ct = host-computed constant of a discrete observation (log binomial
  * coefficient, -lgamma(k+1)); [lo, hi] = Uniform bounds (constants). */
+/* mmb_ir_lp's Normal with log(sigma) supplied (lb = mmb_log(b)): the generated kernels form it
+   once for all the elements a lane evaluates when sigma does not depend on the element */
+MMB_HD double mmb_ir_normal_lb(double x, double a, double b, double lb) {
+  if (x != x) return -__builtin_inf();
+  const double z = (x - a) / b;
+  return -(z * z + MMB_LOG2PI) / 2.0 - lb;
+}
+
 MMB_HD double mmb_ir_lp(int fam, double x, double a, double b, double ct, int tr, double lo, double hi) {
   const double NINF = -__builtin_inf(), INF = __builtin_inf();
   switch (fam) {
