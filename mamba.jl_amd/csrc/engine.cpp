@@ -95,7 +95,9 @@ struct mmb_engine {
   unsigned long long* lg_ngrad = nullptr;
   int32_t* d_cperm = nullptr;  // lane-group slot -> chain of the 32-lane sweep kernels (order_chains)
   bool cperm_identity = true;
-  bool order_fresh = false;    // d_cperm was computed from the current flags (after the last window)
+  bool order_fresh = false;    // d_cperm holds a table computed after a window (a host write of the
+                               // tune state clears it)
+  int64_t order_iter = 0;      // the iteration whose flags d_cperm was computed from
   unsigned long long* d_nstat = nullptr;  // NUTS {updates, depth-cap hits, depth sum}, Slice overflows
                                           // since init_chains
   unsigned long long slice_overflows = 0;  // d_nstat[3] as last reported by mmb_run
@@ -1218,6 +1220,11 @@ static int order_chains(mmb_engine* e) {
   return 0;
 }
 
+static int64_t order_every() {
+  const char* s = std::getenv("MMB_ORDER_EVERY");
+  return (s && std::atoi(s) > 0) ? std::atoi(s) : 64;
+}
+
 // Launch widths of a window: ceil(iters / W) launches of equal length (+-1), so a window of 20
 // iterations at W = 16 runs 10 + 10 instead of 16 + 4 (a short launch pays the launch tail on
 // few iterations)
@@ -1439,9 +1446,10 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
     }
   }
   if (e->model == MMB_MODEL_LOGISTIC) return run_logistic(e, a, (want && nk > 0) ? e->d_draws : nullptr, kept0, nk, want);
-  if (a->iters > 0 && !e->order_fresh) {  // else computed right after the previous window
+  if (a->iters > 0 && !e->order_fresh) {  // else computed right after a previous window
     int orc = order_chains(e);
     if (orc) return orc;
+    e->order_iter = it0;
   }
   SweepArgs A;
   fill_args(e, A);
@@ -1482,12 +1490,17 @@ int mmb_run(mmb_engine* e, const mmb_run_args* a) {
     e->launches += 1;
     e->units += (int64_t)w * e->K;
   }
-  if (a->iters > 0) {
+  if (a->iters > 0 && (!e->order_fresh || it0 + a->iters - e->order_iter >= order_every())) {
     // the next window's order from this window's final flags, queued behind its last launch so
-    // it runs while the host is between windows (a host write of the tune state invalidates it)
+    // it runs while the host is between windows (a host write of the tune state invalidates it).
+    // The classes persist -- a chain's factor-valid flag is set by its first full-rank update and
+    // kept -- so a table less than MMB_ORDER_EVERY iterations old is kept: any table gives the
+    // same results, only the pairing could lag a class change (the kernel is ~21 us, ~1 % of a
+    // 20-iteration window)
     int orc = order_chains(e);
     if (orc) return orc;
     e->order_fresh = true;
+    e->order_iter = it0 + a->iters;
   }
   if (a->time_kernels) {  // per-launch device time, summed after the window (no per-launch sync)
     HIPCHK(e, hipEventSynchronize(e->evpool[2 * nl - 1]));

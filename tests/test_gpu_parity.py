@@ -134,6 +134,25 @@ def test_amm_stats_match_oracle(mamba, oracle, case, monkeypatch):
         assert 0.15 < sg[1]["full_rank"] / sg[1]["updates"] < 0.8
 
 
+def test_chain_order_refresh_interval(mamba, monkeypatch):
+    """The table is recomputed after a window only once MMB_ORDER_EVERY (default 64) iterations
+    have passed since the last one (the classes persist); a host write of the tune state forces a
+    fresh one before the next window."""
+    m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
+    init = mamba.model.rats_init_ls(16384, seed=1000)[:256]
+    monkeypatch.delenv("MMB_ORDER_EVERY", raising=False)
+    eng = mamba.Engine(m)
+    eng.init_chains(init, seed=7)
+    eng.run(100, burnin=0, thin=2, draws=False)   # >= 64: recomputed after the window
+    t100 = eng.chain_order().copy()
+    eng.run(30, burnin=0, thin=2, draws=False)    # 30 < 64: kept
+    np.testing.assert_array_equal(eng.chain_order(), t100)
+    eng.run(40, burnin=0, thin=2, draws=False)    # 70 since: recomputed (a sort of the current classes)
+    t170 = eng.chain_order()
+    assert sorted(t170.tolist()) == list(range(256))
+    eng.close()
+
+
 def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
     """engine.cpp order_chains pairs chains of one factor-validity class in a wavefront before
     every window (the second window below runs permuted: the first set the flags).  The table is
@@ -144,6 +163,7 @@ def test_chain_order_does_not_change_results(mamba, oracle, monkeypatch):
     m = rats(mamba, mamba.model.rats_scheme_gibbs_amm())
     init = mamba.model.rats_init_ls(16384, seed=1000)[:600]
     out = {}
+    monkeypatch.setenv("MMB_ORDER_EVERY", "1")  # a fresh table after every window (checked below)
     for mode in ("ordered", "descending", "balanced", "identity"):
         monkeypatch.setenv("MMB_ORDER_MODE", {"descending": "1", "balanced": "2"}.get(mode, "0"))
         if mode == "identity":
