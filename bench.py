@@ -48,11 +48,11 @@ sys.path.insert(0, ROOT)
 CHAINS_PER_GPU = 16384
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (spec, dense)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r4_rats_gibbs_amm_hbm_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5_rats_gibbs_amm_hbm_traffic.json")
 F64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak (spec)
 # FP64 VALU lane-flops per chain-update of the reference Slice+AMWG scheme (its binding roofline,
 # SURVEY §8(d) row 3'), from the committed rocprofv3 SQ_INSTS_VALU_*_F64 pass
-VALU_FILE = os.path.join(ROOT, "profiles", "r4_rats_reference_valu_flops.json")
+VALU_FILE = os.path.join(ROOT, "profiles", "r5_rats_reference_valu_flops.json")
 
 
 def parse():
