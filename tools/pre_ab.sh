@@ -1,4 +1,6 @@
 #!/bin/bash
+# Sensitivity of the driver's 20-step window to the untimed AMM pre-run and the warm-up length
+# (bench.py --adapt-prerun / --warmup): one bench line per setting, kernel ms per step printed.
 set -e
 mkdir -p gpurun_out/pre
 for cfg in "128 5" "512 5" "128 100" "2000 5" "128 5" "512 5"; do
