@@ -158,6 +158,25 @@ def test_ir_rats_reference_scheme_gpu_vs_oracle(mamba, oracle, monkeypatch):
     np.testing.assert_array_equal(dg2, dg)
 
 
+@pytest.mark.parametrize("variant", ["slice_nc4", "logf_call", "slice_exact"])
+def test_ir_generator_variants(mamba, oracle, variant, monkeypatch):
+    """The specialised kernel's code-generation switches change instruction streams, not draws:
+    four Slice candidates per round instead of two (MMB_IR_SLICE_NC=4: four virtual lanes, three
+    cross-lane butterfly levels), logf called instead of inlined (MMB_IR_LOGF_INLINE=0), and the
+    sequential shrink loop (MMB_SLICE_EXACT=1) -- rats via the IR with the reference scheme equals
+    the oracle bit for bit in each (each variant compiles its own kernel on first use)."""
+    env = {"slice_nc4": ("MMB_IR_SLICE_NC", "4"), "logf_call": ("MMB_IR_LOGF_INLINE", "0"),
+           "slice_exact": ("MMB_SLICE_EXACT", "1")}[variant]
+    monkeypatch.setenv(*env)
+    inits = [{**mamba.model.RATS_INITS[k % 2], "y": mamba.model.RATS_Y} for k in range(64)]
+    m = mamba.ir.rats_model().setinputs(mamba.ir.rats_inputs()).setsamplers(mamba.model.rats_scheme_reference())
+    V = m.init_matrix(inits, 64)
+    eng, dg, st, do = run_both(mamba, oracle, m, V, 40, 10, 2)
+    np.testing.assert_array_equal(dg, do)
+    np.testing.assert_array_equal(eng.values(), st["values"])
+    np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
+
+
 @pytest.mark.parametrize("name", ["seeds", "pumps", "surgical", "dyes", "salm", "blocker"])
 def test_ir_published_summaries(mamba, name):
     """Posterior means of the reference's example runs reproduced by 2048 chains of the same run
