@@ -421,13 +421,14 @@ def test_logistic_nuts_parity(mamba, oracle):
     np.testing.assert_array_equal(eng.tune(), st["tune"][:, :st["tl"]])
 
 
-@pytest.mark.parametrize("grad", ["analytic", "forward"])
+@pytest.mark.parametrize("grad", ["analytic", "forward", "hmc", "mala"])
 def test_logistic_split_identical(mamba, monkeypatch, grad):
     """A window runs its chains as independent parts on their own streams (engine.cpp
     run_logistic): draws, state, tuning and gradient counts identical to one stream for 2 and 3
     parts (unequal), at a width where the group-mode (fold) gradient kernel runs."""
-    m, _ = logistic(mamba, 1000, 50, [mamba.NUTS("beta", dtype=grad)])
-    K = 1500 if grad == "analytic" else 301
+    sch = {"hmc": [mamba.HMC("beta", 0.01, 7, dtype="analytic")], "mala": [mamba.MALA("beta", 2e-4, dtype="analytic")]}
+    m, _ = logistic(mamba, 1000, 50, sch.get(grad) or [mamba.NUTS("beta", dtype=grad)])
+    K = 301 if grad == "forward" else 1500
     init = np.random.default_rng(21).normal(0.0, 0.1, (K, 50))
     out = []
     for split in ("1", "2", "3"):
